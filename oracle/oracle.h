@@ -1,0 +1,76 @@
+// TEST INFRASTRUCTURE ONLY — the CPU oracle for droplet_visual_odometry_amd.
+//
+// A plain C++17 restatement of the OpenCV operators the reference's hot path
+// calls (scripts/visual_odometry_v3.py:373 detectAndCompute, :219 BFMatcher.match,
+// :297 findEssentialMat, :303 recoverPose, :265 triangulatePoints).  OpenCV is a
+// third-party dependency that is neither vendored in the reference nor installed
+// here, so every function below restates OpenCV 4.x's published
+// algorithm; each cites the reference call site it serves and the OpenCV routine
+// it follows.  Parity status: PARTIALLY PINNED — see DESIGN.md §3 (KAT-1 keypoint
+// arithmetic from scripts/back_up_files/frame_extraction_notes.txt:6-7, analytic
+// geometry KATs); bit-level OpenCV parity is unpinned because OpenCV is absent.
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+// this library.  The product (droplet_visual_odometry_amd) never links it.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Same 28-byte layout as cv::KeyPoint's python-visible fields and dvo_keypoint.
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} ora_keypoint;
+
+// ---- ORB (cv::ORB_create() defaults, nfeatures variable) -------------------
+int ora_orb_level_sizes(int w, int h, int nlevels, int* sizes /*2*nlevels*/);
+int ora_orb_features_per_level(int nfeatures, int nlevels, int* out);
+// Pyramid (unblurred when blurred==0, else after GaussianBlur(7x7, sigma 2)).
+// out: levels packed back to back, each w_l*h_l bytes.
+int ora_orb_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels,
+                    int blurred, uint8_t* out);
+// FAST-9/16 with non-max suppression on one image: (x, y, score) triples in
+// raster order.
+int ora_fast(const uint8_t* img, int w, int h, int stride, int threshold,
+             int32_t* xys, int cap, int* n);
+// KeyPointsFilter::retainBest on a response array; perm gets the permutation
+// applied (perm[i] = original index now at i); returns the new size.
+int ora_retain_best(const float* resp, int n, int n_points, int32_t* perm);
+// Restated libstdc++ introselect with an overridable depth limit (-1 = default);
+// used to pin the GPU's parallel emulation including the heap-select path.
+int ora_retain_best_depth(const float* resp, int n, int n_points, int depth, int32_t* perm);
+int ora_orb_detect_and_compute(const uint8_t* img, int w, int h, int stride,
+                               int nfeatures, ora_keypoint* kps, uint8_t* desc,
+                               int cap, int* n_out);
+
+// ---- BFMatcher(NORM_HAMMING, crossCheck) ------------------------------------
+// mode 0: no cross check, 1: OpenCV 4.x mutual check, 2: OpenCV 3.x reverse-only.
+int ora_bf_match_hamming(const uint8_t* dq, int nq, const uint8_t* dt, int nt,
+                         int mode, int32_t* qidx, int32_t* tidx, float* dist,
+                         int* m_out);
+
+// ---- findEssentialMat(RANSAC) / recoverPose / triangulatePoints -------------
+// E_out holds up to 10 stacked 3x3 models (only when m == 5); *rows = 3*k.
+// Returns 0 on success, <0 on failure (E empty).
+int ora_find_essential(const double* p1, const double* p2, int m, const double* K,
+                       double prob, double threshold, int max_iters,
+                       double* E_out, int* rows, uint8_t* mask, int* iters_run);
+int ora_recover_pose(const double* E, const double* p1, const double* p2, int m,
+                     const double* K, double dist_thresh, const uint8_t* mask_in,
+                     double* R, double* t, uint8_t* mask_out, int* good);
+// x1, x2: 2 x k row-major (row 0 = x, row 1 = y).  X: 4 x k row-major.
+int ora_triangulate(const double* P1, const double* P2, const double* x1,
+                    const double* x2, int k, double* X);
+// The 5-point kernel on 5 normalised correspondences; models: up to 10 x 9.
+int ora_five_point(const double* p1, const double* p2, double* models, int* n);
+// Helpers exposed for unit KATs.
+int ora_jacobi_svd(double* At, int m, int n, int n1, double* W, double* Vt);
+int ora_solve_poly(const double* coeffs, int n, int max_iters, double* roots /*2n*/);
+int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
+
+#ifdef __cplusplus
+}
+#endif

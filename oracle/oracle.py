@@ -1,0 +1,241 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front end of the CPU oracle.
+
+Wraps ``oracle/build/libdvo_oracle.so`` (built by ``oracle/Makefile``), the C++
+restatement of the OpenCV operators on the reference's hot path
+(scripts/visual_odometry_v3.py:297-306, :373, :219, :265; see oracle.h).
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg import
+this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libdvo_oracle.so")
+_lib = None
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+_kpp = np.ctypeslib.ndpointer(KEYPOINT_DTYPE, flags="C_CONTIGUOUS")
+_ip = ctypes.POINTER(ctypes.c_int)
+_c = ctypes.c_int
+_d = ctypes.c_double
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        sig = {
+            "ora_orb_level_sizes": [_c, _c, _c, _i32p],
+            "ora_orb_features_per_level": [_c, _c, _i32p],
+            "ora_orb_pyramid": [_u8p, _c, _c, _c, _c, _c, _u8p],
+            "ora_fast": [_u8p, _c, _c, _c, _c, _i32p, _c, _ip],
+            "ora_retain_best": [_f32p, _c, _c, _i32p],
+            "ora_retain_best_depth": [_f32p, _c, _c, _c, _i32p],
+            "ora_orb_detect_and_compute": [_u8p, _c, _c, _c, _c, _kpp, _u8p, _c, _ip],
+            "ora_bf_match_hamming": [_u8p, _c, _u8p, _c, _c, _i32p, _i32p, _f32p, _ip],
+            "ora_find_essential": [_f64p, _f64p, _c, _f64p, _d, _d, _c, _f64p, _ip, _u8p, _ip],
+            "ora_recover_pose": [_f64p, _f64p, _f64p, _c, _f64p, _d, ctypes.c_void_p, _f64p, _f64p, _u8p, _ip],
+            "ora_triangulate": [_f64p, _f64p, _f64p, _f64p, _c, _f64p],
+            "ora_five_point": [_f64p, _f64p, _f64p, _ip],
+            "ora_jacobi_svd": [_f64p, _c, _c, _c, _f64p, _f64p],
+            "ora_solve_poly": [_f64p, _c, _c, _f64p],
+            "ora_ransac_update_num_iters": [_d, _d, _c, _c],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def level_sizes(w, h, nlevels=8):
+    out = np.zeros(2 * nlevels, np.int32)
+    lib().ora_orb_level_sizes(w, h, nlevels, out)
+    return [(int(out[2 * l]), int(out[2 * l + 1])) for l in range(nlevels)]
+
+
+def features_per_level(nfeatures, nlevels=8):
+    out = np.zeros(nlevels, np.int32)
+    lib().ora_orb_features_per_level(nfeatures, nlevels, out)
+    return out.tolist()
+
+
+def pyramid(img, nlevels=8, blurred=False):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    sizes = level_sizes(w, h, nlevels)
+    out = np.zeros(sum(a * b for a, b in sizes), np.uint8)
+    lib().ora_orb_pyramid(img, w, h, w, nlevels, int(blurred), out)
+    levels, off = [], 0
+    for lw, lh in sizes:
+        levels.append(out[off:off + lw * lh].reshape(lh, lw))
+        off += lw * lh
+    return levels
+
+
+def fast(img, threshold=20):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = (w // 2 + 1) * (h // 2 + 1)
+    buf = np.zeros(3 * cap, np.int32)
+    n = ctypes.c_int()
+    rc = lib().ora_fast(img, w, h, w, threshold, buf, cap, ctypes.byref(n))
+    assert rc == 0
+    return buf[:3 * n.value].reshape(-1, 3)
+
+
+def retain_best(resp, n_points, depth=None):
+    resp = np.ascontiguousarray(resp, np.float32)
+    perm = np.zeros(max(len(resp), 1), np.int32)
+    if depth is None:
+        k = lib().ora_retain_best(resp, len(resp), n_points, perm)
+    else:
+        k = lib().ora_retain_best_depth(resp, len(resp), n_points, depth, perm)
+    return perm[:k]
+
+
+def detect_and_compute(img, nfeatures=500):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = 4 * nfeatures + 1024
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_int()
+    rc = lib().ora_orb_detect_and_compute(img, w, h, w, nfeatures, kps, desc, cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def bf_match(dq, dt, mode=1):
+    dq = np.ascontiguousarray(dq, np.uint8)
+    dt = np.ascontiguousarray(dt, np.uint8)
+    nq, nt = len(dq), len(dt)
+    q = np.zeros(max(nq, 1), np.int32)
+    t = np.zeros(max(nq, 1), np.int32)
+    d = np.zeros(max(nq, 1), np.float32)
+    m = ctypes.c_int()
+    lib().ora_bf_match_hamming(dq.reshape(-1) if nq else np.zeros(32, np.uint8), nq,
+                               dt.reshape(-1) if nt else np.zeros(32, np.uint8), nt, mode, q, t, d,
+                               ctypes.byref(m))
+    k = m.value
+    return q[:k].copy(), t[:k].copy(), d[:k].copy()
+
+
+def find_essential(p1, p2, K, prob=0.999, threshold=1.0, max_iters=1000):
+    p1 = np.ascontiguousarray(p1, np.float64).reshape(-1)
+    p2 = np.ascontiguousarray(p2, np.float64).reshape(-1)
+    m = len(p1) // 2
+    E = np.zeros(90, np.float64)
+    rows = ctypes.c_int()
+    mask = np.zeros(max(m, 1), np.uint8)
+    iters = ctypes.c_int()
+    rc = lib().ora_find_essential(p1, p2, m, np.ascontiguousarray(K, np.float64).reshape(-1), prob, threshold,
+                                  max_iters, E, ctypes.byref(rows), mask, ctypes.byref(iters))
+    if rc != 0:
+        return None, None, iters.value
+    return E[:rows.value * 3].reshape(rows.value, 3).copy(), mask[:m].copy(), iters.value
+
+
+def recover_pose(E, p1, p2, K, dist_thresh=50.0, mask=None):
+    p1 = np.ascontiguousarray(p1, np.float64).reshape(-1)
+    p2 = np.ascontiguousarray(p2, np.float64).reshape(-1)
+    m = len(p1) // 2
+    R = np.zeros(9, np.float64)
+    t = np.zeros(3, np.float64)
+    mo = np.zeros(max(m, 1), np.uint8)
+    good = ctypes.c_int()
+    mk = None
+    if mask is not None:
+        mask = np.ascontiguousarray(mask, np.uint8).reshape(-1)
+        mk = mask.ctypes.data_as(ctypes.c_void_p)
+    lib().ora_recover_pose(np.ascontiguousarray(E, np.float64).reshape(-1), p1, p2, m,
+                           np.ascontiguousarray(K, np.float64).reshape(-1), dist_thresh, mk, R, t, mo,
+                           ctypes.byref(good))
+    return good.value, R.reshape(3, 3), t.reshape(3, 1), mo[:m].copy()
+
+
+def triangulate(P1, P2, x1, x2):
+    x1 = np.ascontiguousarray(x1, np.float64)
+    x2 = np.ascontiguousarray(x2, np.float64)
+    k = x1.shape[1]
+    X = np.zeros(4 * k, np.float64)
+    lib().ora_triangulate(np.ascontiguousarray(P1, np.float64).reshape(-1),
+                          np.ascontiguousarray(P2, np.float64).reshape(-1), x1.reshape(-1), x2.reshape(-1), k, X)
+    return X.reshape(4, k)
+
+
+def five_point(q1, q2):
+    models = np.zeros(90, np.float64)
+    n = ctypes.c_int()
+    lib().ora_five_point(np.ascontiguousarray(q1, np.float64).reshape(-1),
+                         np.ascontiguousarray(q2, np.float64).reshape(-1), models, ctypes.byref(n))
+    return models[:9 * n.value].reshape(n.value, 3, 3).copy()
+
+
+def jacobi_svd(A, full_u=False):
+    """SVD of A (rows x cols) the way cv::SVD::compute does it (m >= n case only)."""
+    A = np.asarray(A, np.float64)
+    rows, cols = A.shape
+    assert rows >= cols
+    At = np.ascontiguousarray(A.T).reshape(-1).copy()
+    W = np.zeros(cols)
+    Vt = np.zeros(cols * cols)
+    lib().ora_jacobi_svd(At, rows, cols, cols if full_u else 0, W, Vt)
+    return W, At.reshape(cols, rows).T, Vt.reshape(cols, cols)
+
+
+def solve_poly(coeffs, max_iters=300):
+    coeffs = np.ascontiguousarray(coeffs, np.float64)
+    n = len(coeffs) - 1
+    roots = np.zeros(2 * n)
+    k = lib().ora_solve_poly(coeffs, n, max_iters, roots)
+    return roots[:2 * k].reshape(k, 2)
+
+
+def ransac_update_num_iters(p, ep, model_points, max_iters):
+    return lib().ora_ransac_update_num_iters(p, ep, model_points, max_iters)
+
+
+def keypoints_to_points(kps):
+    return np.stack([kps["x"], kps["y"]], axis=1).astype(np.float32)
+
+
+def pair_pose(img_prev, img_cur, K, nfeatures=500, max_iters=1000, kp_prev=None):
+    """The full per-pair hot path (v3:384-408 minus the host pose tail) on the CPU."""
+    if kp_prev is None:
+        kp_prev = detect_and_compute(img_prev, nfeatures)
+    kp1, d1 = kp_prev
+    kp2, d2 = detect_and_compute(img_cur, nfeatures)
+    q, t, d = bf_match(d1, d2, 1)
+    order = np.argsort(d, kind="stable")  # sorted(matches, key=distance), v3:221
+    q, t = q[order], t[order]
+    p1 = keypoints_to_points(kp1[q]).astype(np.float64)
+    p2 = keypoints_to_points(kp2[t]).astype(np.float64)
+    E, mask, iters = find_essential(p1, p2, K, max_iters=max_iters)
+    out = dict(kp_prev=kp1, kp_cur=kp2, desc_cur=d2, q=q, t=t, p1=p1, p2=p2, E=E, iters=iters)
+    if E is None or E.shape[0] != 3:
+        out.update(R=None, t_unit=None, good=0)
+        return out
+    good, R, tv, _ = recover_pose(E, p1, p2, K)
+    out.update(R=R, t_unit=tv, good=good)
+    return out
