@@ -1,0 +1,96 @@
+"""Build libdvo_hip.so (the MI355X kernels + C ABI) in-tree with hipcc for gfx950.
+
+Numerics flags are part of the product contract:
+  -ffp-contract=off                          no FMA contraction: every float/double
+                                             expression rounds like the CPU oracle
+  -fhip-fp32-correctly-rounded-divide-sqrt   IEEE f32 division / sqrt
+The shared object links the HIP runtime by the unversioned soname
+``libamdhip64.so``; when PyTorch-ROCm is loaded first (the bench, the tests)
+the dynamic linker reuses torch's copy, so torch tensors and the library share
+one HIP runtime and one device address space.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libdvo_hip.so")
+ARCH = os.environ.get("DVO_OFFLOAD_ARCH", "gfx950")
+
+CXXFLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    "-ffp-contract=off", "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
+]
+
+
+def _torch_lib_dir():
+    try:
+        import torch  # noqa: F401  (location only; the library never calls torch)
+        d = os.path.join(os.path.dirname(torch.__file__), "lib")
+        if os.path.exists(os.path.join(d, "libamdhip64.so")):
+            return d
+    except Exception:
+        pass
+    return None
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+
+
+def _stale(objs):
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
+        os.path.join(HERE, "..", "include", "dvo.h"), os.path.join(HERE, "..", "data", "orb_bit_pattern_31.inc"),
+        __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    srcs = sources()
+    objs = [os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o") for s in srcs]
+    if not force and not _stale(objs):
+        return LIB
+
+    def compile_one(pair):
+        src, obj = pair
+        lang = ["-x", "hip"]
+        cmd = [hipcc, *lang, *CXXFLAGS, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        return r.stderr
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        for warn in ex.map(compile_one, zip(srcs, objs)):
+            if warn and verbose:
+                print(warn)
+    tl = _torch_lib_dir()
+    link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp", *objs]
+    if tl:
+        # resolve -lamdhip64 to torch's soname-less copy first -> NEEDED libamdhip64.so
+        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp", *objs,
+                f"-L{tl}", f"-Wl,-rpath,{tl}", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(link, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,671 @@
+// C-ABI of libdvo_hip.so (include/dvo.h): contexts, ORB plans, device buffers
+// and the per-call entry points that replace the reference's OpenCV calls.
+// Host code only sizes buffers and moves bytes; every computation runs in the
+// HIP kernels of orb.hip, match.hip and geometry.hip.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dvo_internal.h"
+
+using namespace dvo;
+
+struct dvo_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // grow-only scratch for the per-call entry points
+    std::vector<std::pair<void*, size_t>> scratch;
+    dvo_stream* call_stream = nullptr;  // cached plan for detectAndCompute
+    int call_w = 0, call_h = 0, call_nf = 0;
+};
+
+struct dvo_stream {
+    dvo_ctx* ctx = nullptr;
+    dvo_stream_config cfg{};
+    Plan plan{};
+    Buffers buf{};
+    std::vector<void*> allocs;
+    uint8_t* d_frames = nullptr;  // per-call upload slab (max_frames images)
+    int last_nframes = 0;
+    hipStream_t hs = nullptr;
+};
+
+namespace {
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            if (ctx) ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);       \
+            return DVO_EHIP;                                                             \
+        }                                                                                \
+    } while (0)
+
+int fail(dvo_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int cv_round_f(float v) { return (int)lrintf(v); }
+
+// orb.cpp computeKeyPoints: features per level (float arithmetic as OpenCV).
+void features_per_level(int nfeatures, int nlevels, int* out) {
+    const double sf = (double)1.2f;
+    float factor = (float)(1.0 / sf);
+    float ndesired = nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nlevels));
+    int sum = 0;
+    for (int l = 0; l < nlevels - 1; ++l) {
+        out[l] = cv_round_f(ndesired);
+        sum += out[l];
+        ndesired *= factor;
+    }
+    out[nlevels - 1] = std::max(nfeatures - sum, 0);
+}
+
+Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
+    Plan p{};
+    p.w = w;
+    p.h = h;
+    p.nlevels = kMaxLevels;
+    p.nfeatures = nfeatures;
+    p.fast_threshold = fast_threshold;
+    int nper[kMaxLevels];
+    features_per_level(nfeatures, kMaxLevels, nper);
+    int64_t pyr = 0, blur = 0, bcand = 0, cand = 0;
+    int bands = 0, tiles = 0;
+    for (int l = 0; l < kMaxLevels; ++l) {
+        LevelGeom& G = p.L[l];
+        G.scale = (float)std::pow((double)1.2f, (double)l);  // getScale
+        float inv = 1.0f / G.scale;
+        G.w = l == 0 ? w : cv_round_f(w * inv);
+        G.h = l == 0 ? h : cv_round_f(h * inv);
+        G.nper = nper[l];
+        G.pyr_off = l == 0 ? 0 : pyr;
+        if (l > 0) pyr += (int64_t)G.w * G.h;
+        G.blur_off = blur;
+        blur += (int64_t)G.w * G.h;
+        const bool usable = G.w > 2 * kBorder && G.h > 2 * kBorder;
+        const int rows = usable ? G.h - 2 * kBorder : 0;
+        const int wc = usable ? G.w - 2 * kBorder : 0;
+        G.nbands = (rows + kBandRows - 1) / kBandRows;
+        G.band_base = bands;
+        bands += G.nbands;
+        G.band_cap = (kBandRows / 2) * ((wc + 1) / 2) + 4;
+        G.band_cand_off = bcand;
+        bcand += (int64_t)G.nbands * G.band_cap;
+        G.cand_cap = G.nbands * G.band_cap + 4;
+        G.cand_off = cand;
+        cand += G.cand_cap;
+        G.tiles_x = (G.w + 63) / 64;
+        G.tiles_y = (G.h + 15) / 16;
+        G.tile_base = tiles;
+        tiles += G.tiles_x * G.tiles_y;
+    }
+    p.pyr_stride = (pyr + 255) & ~(int64_t)255;
+    p.blur_stride = (blur + 255) & ~(int64_t)255;
+    p.total_bands = bands;
+    p.band_cand_stride = (bcand + 63) & ~(int64_t)63;
+    p.cand_stride = (cand + 63) & ~(int64_t)63;
+    p.total_tiles = tiles;
+    p.kp_cap = ((nfeatures + 256) + 63) & ~63;
+    return p;
+}
+
+int check_orb_params(dvo_ctx* ctx, const dvo_orb_params* o) {
+    if (!o) return fail(ctx, DVO_EINVAL, "null ORB parameters");
+    if (o->nfeatures <= 0 || o->nfeatures > 7680) return fail(ctx, DVO_EINVAL, "nfeatures out of range (1..7680)");
+    if (o->scale_factor != 1.2f || o->nlevels != 8 || o->edge_threshold != 31 || o->first_level != 0 || o->wta_k != 2 ||
+        o->score_type != 0 || o->patch_size != 31)
+        return fail(ctx, DVO_EINVAL,
+                    "only cv.ORB_create() defaults (scaleFactor 1.2, nlevels 8, edgeThreshold 31, firstLevel 0, "
+                    "WTA_K 2, HARRIS_SCORE, patchSize 31) are implemented");
+    if (o->fast_threshold < 0 || o->fast_threshold > 255) return fail(ctx, DVO_EINVAL, "fastThreshold out of range");
+    return DVO_OK;
+}
+
+template <class T>
+int dalloc(dvo_stream* s, T** p, size_t n) {
+    dvo_ctx* ctx = s->ctx;
+    void* q = nullptr;
+    HIP_TRY(hipMalloc(&q, n * sizeof(T) + 256));
+    s->allocs.push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return DVO_OK;
+}
+
+// grow-only per-context scratch slot
+int scratch(dvo_ctx* ctx, int slot, size_t bytes, void** out) {
+    if ((int)ctx->scratch.size() <= slot) ctx->scratch.resize(slot + 1, {nullptr, 0});
+    auto& e = ctx->scratch[slot];
+    if (e.second < bytes) {
+        if (e.first) HIP_TRY(hipFree(e.first));
+        e.first = nullptr;
+        e.second = 0;
+        size_t nb = bytes < 4096 ? 4096 : bytes + bytes / 4;
+        HIP_TRY(hipMalloc(&e.first, nb));
+        e.second = nb;
+    }
+    *out = e.first;
+    return DVO_OK;
+}
+
+StreamParams params_of(dvo_stream* s, const uint8_t* frames, int nframes, int64_t frame_stride, int pitch) {
+    StreamParams P{};
+    P.plan = s->plan;
+    P.buf = s->buf;
+    P.frames = frames;
+    P.frame_stride = frame_stride;
+    P.in_pitch = pitch;
+    P.nframes = nframes;
+    return P;
+}
+
+GeomArgs stream_geom(dvo_stream* s) {
+    GeomArgs g{};
+    const dvo_stream_config& c = s->cfg;
+    g.pts_f = s->buf.pts;
+    g.m_arr = s->buf.nmatch;
+    g.pts_stride = s->plan.kp_cap;
+    g.fx = c.K[0];
+    g.fy = c.K[4];
+    g.cx = c.K[2];
+    g.cy = c.K[5];
+    g.prob = c.prob;
+    g.threshold = c.threshold;
+    g.max_iters = c.max_iters;
+    g.dist_thresh = c.dist_thresh;
+    g.npts = s->buf.npts;
+    g.models = s->buf.models;
+    g.E = s->buf.E;
+    g.info = s->buf.info;
+    g.Rt = s->buf.Rt;
+    g.good = s->buf.good;
+    return g;
+}
+
+int stream_alloc(dvo_stream* s) {
+    const int F = s->cfg.max_frames;
+    const Plan& p = s->plan;
+    Buffers& b = s->buf;
+    const int cap = p.kp_cap;
+    int rc;
+#define A(ptr, n)                              \
+    if ((rc = dalloc(s, &(ptr), (size_t)(n)))) \
+        return rc;
+    A(b.pyr, (size_t)F * p.pyr_stride);
+    A(b.blur, (size_t)F * p.blur_stride);
+    A(b.band_cnt, (size_t)F * (p.total_bands + 1));
+    A(b.band_cand, (size_t)F * p.band_cand_stride);
+    A(b.cand, (size_t)F * p.cand_stride);
+    A(b.resp, (size_t)F * p.cand_stride);
+    A(b.sel_tmp, (size_t)F * 2 * p.cand_stride);
+    A(b.cnt1, (size_t)F * kMaxLevels);
+    A(b.cnt2, (size_t)F * kMaxLevels);
+    A(b.kps, (size_t)F * cap);
+    A(b.desc, (size_t)F * cap * 32);
+    A(b.nkp, (size_t)F);
+    A(b.nn, (size_t)2 * F * cap);
+    A(b.mq, (size_t)F * cap);
+    A(b.mt, (size_t)F * cap);
+    A(b.md, (size_t)F * cap);
+    A(b.nmatch, (size_t)F);
+    A(b.pts, (size_t)F * cap * 4);
+    A(b.npts, (size_t)F * cap * 4);
+    A(b.models, (size_t)F * kChunk * 90);
+    A(b.status, (size_t)F);
+    A(b.E, (size_t)F * 90);
+    A(b.info, (size_t)F * 4);
+    A(b.Rt, (size_t)F * 12);
+    A(b.good, (size_t)F);
+    A(s->d_frames, (size_t)F * s->cfg.width * s->cfg.height);
+#undef A
+    return DVO_OK;
+}
+
+dvo_orb_params default_orb(int nfeatures) {
+    dvo_orb_params o{};
+    o.nfeatures = nfeatures;
+    o.scale_factor = 1.2f;
+    o.nlevels = 8;
+    o.edge_threshold = 31;
+    o.first_level = 0;
+    o.wta_k = 2;
+    o.score_type = 0;
+    o.patch_size = 31;
+    o.fast_threshold = 20;
+    return o;
+}
+
+int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, int pitch, dvo_pair_record* d_rec,
+               bool detect_only) {
+    dvo_ctx* ctx = s->ctx;
+    StreamParams P = params_of(s, d_frames, n, fstride, pitch);
+    HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
+    HIP_TRY(launch_orb(P, s->hs));
+    s->last_nframes = n;
+    if (detect_only || n < 2) return DVO_OK;
+    HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs));
+    GeomArgs g = stream_geom(s);
+    HIP_TRY(launch_geometry(P, g, d_rec, s->hs));
+    return DVO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dvo_version(void) { return 1; }
+
+int dvo_ctx_create(dvo_ctx** out, int device) {
+    if (!out) return DVO_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DVO_EHIP;
+    if (device < 0 || device >= n) return DVO_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return DVO_EHIP;
+    dvo_ctx* ctx = new dvo_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return DVO_EHIP;
+    }
+    *out = ctx;
+    return DVO_OK;
+}
+
+void dvo_ctx_destroy(dvo_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
+    for (auto& e : ctx->scratch)
+        if (e.first) hipFree(e.first);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* dvo_last_error(const dvo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** out) {
+    if (!ctx || !cfg || !out) return fail(ctx, DVO_EINVAL, "null argument");
+    *out = nullptr;
+    int rc = check_orb_params(ctx, &cfg->orb);
+    if (rc) return rc;
+    if (cfg->width < 8 || cfg->height < 8 || cfg->width >= kMaxW || cfg->height >= kMaxW)
+        return fail(ctx, DVO_EINVAL, "frame size out of range (8..4095)");
+    if (cfg->max_frames < 1) return fail(ctx, DVO_EINVAL, "max_frames < 1");
+    if (cfg->cross_check < 0 || cfg->cross_check > 2) return fail(ctx, DVO_EINVAL, "cross_check must be 0, 1 or 2");
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto s = std::make_unique<dvo_stream>();
+    s->ctx = ctx;
+    s->cfg = *cfg;
+    s->plan = make_plan(cfg->width, cfg->height, cfg->orb.nfeatures, cfg->orb.fast_threshold);
+    if (s->plan.kp_cap > 65535) return fail(ctx, DVO_EINVAL, "too many features");
+    s->hs = ctx->stream;
+    rc = stream_alloc(s.get());
+    if (rc) {
+        for (void* p : s->allocs) hipFree(p);
+        return rc;
+    }
+    *out = s.release();
+    return DVO_OK;
+}
+
+void dvo_stream_destroy(dvo_stream* s) {
+    if (!s) return;
+    hipSetDevice(s->ctx->device);
+    hipStreamSynchronize(s->hs);
+    for (void* p : s->allocs) hipFree(p);
+    delete s;
+}
+
+void* dvo_stream_hip_stream(dvo_stream* s) { return s ? (void*)s->hs : nullptr; }
+
+int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                       dvo_pair_record* d_records) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (n_frames < 1 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range");
+    if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
+    if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
+    HIP_TRY(hipSetDevice(ctx->device));
+    return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false);
+}
+
+int dvo_stream_sync(dvo_stream* s) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    HIP_TRY(hipGetLastError());
+    return DVO_OK;
+}
+
+int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t* desc, int cap, int* n) {
+    if (!s || !n) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (frame < 0 || frame >= s->last_nframes) return fail(ctx, DVO_EINVAL, "frame out of range");
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    int nk = 0, st = 0;
+    HIP_TRY(hipMemcpy(&nk, s->buf.nkp + frame, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&st, s->buf.status + frame, sizeof(int), hipMemcpyDeviceToHost));
+    *n = nk;
+    if (st) return fail(ctx, DVO_ECAP, "keypoint capacity exceeded (Harris ties)");
+    if (nk > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    if (nk > 0) {
+        if (kps)
+            HIP_TRY(hipMemcpy(kps, s->buf.kps + (size_t)frame * s->plan.kp_cap, sizeof(dvo_keypoint) * nk,
+                              hipMemcpyDeviceToHost));
+        if (desc)
+            HIP_TRY(hipMemcpy(desc, s->buf.desc + (size_t)frame * s->plan.kp_cap * 32, 32 * (size_t)nk,
+                              hipMemcpyDeviceToHost));
+    }
+    return DVO_OK;
+}
+
+int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m) {
+    if (!s || !m) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (pair < 0 || pair >= s->last_nframes - 1) return fail(ctx, DVO_EINVAL, "pair out of range");
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    int nm = 0;
+    HIP_TRY(hipMemcpy(&nm, s->buf.nmatch + pair, sizeof(int), hipMemcpyDeviceToHost));
+    *m = nm;
+    if (nm > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    std::vector<int32_t> q(nm), t(nm);
+    std::vector<float> d(nm);
+    const size_t off = (size_t)pair * s->plan.kp_cap;
+    if (nm) {
+        HIP_TRY(hipMemcpy(q.data(), s->buf.mq + off, 4 * (size_t)nm, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(t.data(), s->buf.mt + off, 4 * (size_t)nm, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(d.data(), s->buf.md + off, 4 * (size_t)nm, hipMemcpyDeviceToHost));
+    }
+    for (int i = 0; i < nm; ++i) out[i] = dvo_dmatch{q[i], t[i], 0, d[i]};
+    return DVO_OK;
+}
+
+int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uint8_t* out, int cap) {
+    if (!s || !out) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (frame < 0 || frame >= s->last_nframes || level < 0 || level >= s->plan.nlevels)
+        return fail(ctx, DVO_EINVAL, "frame/level out of range");
+    const LevelGeom& G = s->plan.L[level];
+    if (cap < G.w * G.h) return fail(ctx, DVO_ECAP, "capacity too small");
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    if (blurred) {
+        HIP_TRY(hipMemcpy(out, s->buf.blur + (size_t)frame * s->plan.blur_stride + G.blur_off, (size_t)G.w * G.h,
+                          hipMemcpyDeviceToHost));
+    } else {
+        if (level == 0) return fail(ctx, DVO_EINVAL, "level 0 is the input frame");
+        HIP_TRY(hipMemcpy(out, s->buf.pyr + (size_t)frame * s->plan.pyr_stride + G.pyr_off, (size_t)G.w * G.h,
+                          hipMemcpyDeviceToHost));
+    }
+    return DVO_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const uint8_t* img, int w, int h,
+                               int stride, dvo_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+    if (!ctx) return DVO_EINVAL;
+    int rc = check_orb_params(ctx, params);
+    if (rc) return rc;
+    if (!img || !n_out || stride < w) return fail(ctx, DVO_EINVAL, "bad image buffer");
+    if (w < 8 || h < 8 || w >= kMaxW || h >= kMaxW) return fail(ctx, DVO_EINVAL, "image size out of range (8..4095)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (!ctx->call_stream || ctx->call_w != w || ctx->call_h != h || ctx->call_nf != params->nfeatures ||
+        ctx->call_stream->cfg.orb.fast_threshold != params->fast_threshold) {
+        if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
+        ctx->call_stream = nullptr;
+        dvo_stream_config cfg{};
+        cfg.width = w;
+        cfg.height = h;
+        cfg.max_frames = 2;
+        cfg.orb = *params;
+        cfg.K[0] = cfg.K[4] = cfg.K[8] = 1.0;
+        cfg.prob = 0.999;
+        cfg.threshold = 1.0;
+        cfg.max_iters = 1000;
+        cfg.cross_check = 1;
+        cfg.dist_thresh = 50.0;
+        rc = dvo_stream_create(ctx, &cfg, &ctx->call_stream);
+        if (rc) return rc;
+        ctx->call_w = w;
+        ctx->call_h = h;
+        ctx->call_nf = params->nfeatures;
+    }
+    dvo_stream* s = ctx->call_stream;
+    HIP_TRY(hipMemcpy2DAsync(s->d_frames, w, img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+    rc = run_stream(s, s->d_frames, 1, (int64_t)w * h, w, nullptr, true);
+    if (rc) return rc;
+    return dvo_stream_get_features(s, 0, kps, desc, cap, n_out);
+}
+
+int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int cross_check,
+                         dvo_dmatch* out, int cap, int* m_out) {
+    if (!ctx || !m_out) return DVO_EINVAL;
+    *m_out = 0;
+    if (cross_check < 0 || cross_check > 2) return fail(ctx, DVO_EINVAL, "cross_check must be 0, 1 or 2");
+    if (nq < 0 || nt < 0 || nq > 8192 || nt > 8192)
+        return fail(ctx, DVO_EINVAL, "descriptor count out of range (0..8192)");
+    if (nq == 0 || nt == 0) return DVO_OK;  // BFMatcher returns no matches
+    if (!dq || !dt || !out) return fail(ctx, DVO_EINVAL, "null buffer");
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *bq, *bt, *bnn, *bout, *bm;
+    int rc;
+    if ((rc = scratch(ctx, 0, (size_t)nq * 32, &bq)) || (rc = scratch(ctx, 1, (size_t)nt * 32, &bt)) ||
+        (rc = scratch(ctx, 2, (size_t)(nq + nt) * 4, &bnn)) || (rc = scratch(ctx, 3, (size_t)nq * sizeof(dvo_dmatch), &bout)) ||
+        (rc = scratch(ctx, 4, 64, &bm)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(bq, dq, (size_t)nq * 32, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(bt, dt, (size_t)nt * 32, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_match_pair((const uint8_t*)bq, nq, (const uint8_t*)bt, nt, cross_check, (int32_t*)bnn,
+                              (dvo_dmatch*)bout, (int*)bm, ctx->stream));
+    int m = 0;
+    HIP_TRY(hipMemcpyAsync(&m, bm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *m_out = m;
+    if (m > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    if (m) HIP_TRY(hipMemcpy(out, bout, (size_t)m * sizeof(dvo_dmatch), hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+static int upload_points(dvo_ctx* ctx, const double* p1, const double* p2, int m, void** dpts) {
+    int rc = scratch(ctx, 5, (size_t)(m > 0 ? m : 1) * 32, dpts);
+    if (rc) return rc;
+    std::vector<double> h((size_t)m * 4);
+    for (int i = 0; i < m; ++i) {
+        h[4 * i] = p1[2 * i];
+        h[4 * i + 1] = p1[2 * i + 1];
+        h[4 * i + 2] = p2[2 * i];
+        h[4 * i + 3] = p2[2 * i + 1];
+    }
+    if (m) HIP_TRY(hipMemcpy(*dpts, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    return DVO_OK;
+}
+
+int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int m, const double* K, double prob,
+                           double threshold, int max_iters, double* E, int* e_rows, uint8_t* mask) {
+    if (!ctx || !K || !E || !e_rows) return DVO_EINVAL;
+    *e_rows = 0;
+    if (m < 0 || (m > 0 && (!p1 || !p2))) return fail(ctx, DVO_EINVAL, "bad point arrays");
+    if (!(prob > 0 && prob < 1)) return fail(ctx, DVO_EINVAL, "prob must be in (0, 1)");
+    if (m < 5) return fail(ctx, DVO_EFEWPTS, "fewer than 5 correspondences");
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask;
+    int rc;
+    if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)m * 32, &dn)) ||
+        (rc = scratch(ctx, 7, (size_t)kChunk * 90 * 8, &dmod)) || (rc = scratch(ctx, 8, 90 * 8, &dE)) ||
+        (rc = scratch(ctx, 9, 16, &dinfo)) || (rc = scratch(ctx, 10, (size_t)m, &dmask)))
+        return rc;
+    GeomArgs g{};
+    g.pts_d = (const double*)dpts;
+    g.m_const = m;
+    g.pts_stride = m;
+    g.fx = K[0];
+    g.fy = K[4];
+    g.cx = K[2];
+    g.cy = K[5];
+    g.prob = prob;
+    g.threshold = threshold;
+    g.max_iters = max_iters;
+    g.npts = (double*)dn;
+    g.models = (double*)dmod;
+    g.E = (double*)dE;
+    g.info = (int32_t*)dinfo;
+    g.mask = (uint8_t*)dmask;
+    HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStageRansac, ctx->stream));
+    int info[4];
+    HIP_TRY(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (info[3] != DVO_OK) return fail(ctx, info[3], "findEssentialMat: no model (E is empty)");
+    *e_rows = info[0];
+    HIP_TRY(hipMemcpy(E, dE, sizeof(double) * 3 * info[0], hipMemcpyDeviceToHost));
+    if (mask) HIP_TRY(hipMemcpy(mask, dmask, (size_t)m, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+int dvo_recover_pose(dvo_ctx* ctx, const double* E, int e_rows, const double* p1, const double* p2, int m,
+                     const double* K, double dist_thresh, const uint8_t* mask_in, double* R, double* t,
+                     uint8_t* mask_out, int* good) {
+    if (!ctx || !E || !K || !R || !t || !good) return DVO_EINVAL;
+    if (e_rows != 3) return fail(ctx, DVO_EINVAL, "recoverPose: E must be 3x3 (decomposeEssentialMat reshape)");
+    if (m < 0 || (m > 0 && (!p1 || !p2))) return fail(ctx, DVO_EINVAL, "bad point arrays");
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dpts, *dn, *dE, *dinfo, *dRt, *dgood, *dpick, *dpm, *dmin = nullptr;
+    int rc;
+    const int mm = m > 0 ? m : 1;
+    if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)mm * 32, &dn)) ||
+        (rc = scratch(ctx, 8, 90 * 8, &dE)) || (rc = scratch(ctx, 9, 16, &dinfo)) ||
+        (rc = scratch(ctx, 11, 12 * 8, &dRt)) || (rc = scratch(ctx, 12, 8, &dgood)) ||
+        (rc = scratch(ctx, 13, 8, &dpick)) || (rc = scratch(ctx, 14, (size_t)mm * 4, &dpm)))
+        return rc;
+    if (mask_in) {
+        if ((rc = scratch(ctx, 15, (size_t)mm, &dmin))) return rc;
+        if (m) HIP_TRY(hipMemcpy(dmin, mask_in, (size_t)m, hipMemcpyHostToDevice));
+    }
+    const int info[4] = {3, 0, 0, DVO_OK};
+    HIP_TRY(hipMemcpy(dE, E, 9 * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dinfo, info, sizeof(info), hipMemcpyHostToDevice));
+    GeomArgs g{};
+    g.pts_d = (const double*)dpts;
+    g.m_const = m;
+    g.pts_stride = mm;
+    g.fx = K[0];
+    g.fy = K[4];
+    g.cx = K[2];
+    g.cy = K[5];
+    g.dist_thresh = dist_thresh;
+    g.npts = (double*)dn;
+    g.E = (double*)dE;
+    g.info = (int32_t*)dinfo;
+    g.mask_in = (const uint8_t*)dmin;
+    g.Rt = (double*)dRt;
+    g.good = (int32_t*)dgood;
+    g.pick = (int32_t*)dpick;
+    g.pose_mask = (uint8_t*)dpm;
+    HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStagePose, ctx->stream));
+    double Rt[12];
+    int gd = 0, pick = 0;
+    HIP_TRY(hipMemcpyAsync(Rt, dRt, sizeof(Rt), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&gd, dgood, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&pick, dpick, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::memcpy(R, Rt, 9 * sizeof(double));
+    std::memcpy(t, Rt + 9, 3 * sizeof(double));
+    *good = gd;
+    if (mask_out && m > 0) {
+        std::vector<uint8_t> pm((size_t)m * 4);
+        HIP_TRY(hipMemcpy(pm.data(), dpm, pm.size(), hipMemcpyDeviceToHost));
+        for (int i = 0; i < m; ++i) mask_out[i] = pm[(size_t)i * 4 + pick];
+    }
+    return DVO_OK;
+}
+
+int dvo_triangulate_points(dvo_ctx* ctx, const double* P1, const double* P2, const double* x1, const double* x2,
+                           int k, double* X) {
+    if (!ctx || !P1 || !P2 || !X || k < 0 || (k > 0 && (!x1 || !x2))) return DVO_EINVAL;
+    if (k == 0) return DVO_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dP, *dx, *dX;
+    int rc;
+    if ((rc = scratch(ctx, 16, 24 * 8, &dP)) || (rc = scratch(ctx, 17, (size_t)k * 32, &dx)) ||
+        (rc = scratch(ctx, 18, (size_t)k * 32, &dX)))
+        return rc;
+    double P[24];
+    std::memcpy(P, P1, 12 * sizeof(double));
+    std::memcpy(P + 12, P2, 12 * sizeof(double));
+    HIP_TRY(hipMemcpy(dP, P, sizeof(P), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dx, x1, (size_t)k * 16, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy((char*)dx + (size_t)k * 16, x2, (size_t)k * 16, hipMemcpyHostToDevice));
+    HIP_TRY(launch_triangulate((const double*)dP, (const double*)dx, k, (double*)dX, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(X, dX, (size_t)k * 32, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int32_t* perm, int* k_out) {
+    if (!ctx || !resp || !perm || !k_out || n < 0) return DVO_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dv, *dk, *dt, *dkk;
+    int rc;
+    if ((rc = scratch(ctx, 20, (size_t)(n + 1) * 4, &dv)) || (rc = scratch(ctx, 21, (size_t)(n + 1) * 4, &dk)) ||
+        (rc = scratch(ctx, 22, (size_t)(2 * n + 2) * 4, &dt)) || (rc = scratch(ctx, 23, 8, &dkk)))
+        return rc;
+    std::vector<uint32_t> ids(n);
+    for (int i = 0; i < n; ++i) ids[i] = (uint32_t)i;
+    if (n) {
+        HIP_TRY(hipMemcpy(dv, resp, (size_t)n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(dk, ids.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(launch_test_retain_best((float*)dv, (uint32_t*)dk, (int32_t*)dt, n, n_points, depth, (int*)dkk, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int k = 0;
+    HIP_TRY(hipMemcpy(&k, dkk, sizeof(int), hipMemcpyDeviceToHost));
+    *k_out = k;
+    if (k) HIP_TRY(hipMemcpy(perm, dk, (size_t)k * 4, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+int dvo_test_update_num_iters(dvo_ctx* ctx, double p, const double* ep, int n, int model_points, int max_iters,
+                              int32_t* out) {
+    if (!ctx || !ep || !out || n < 0) return DVO_EINVAL;
+    if (n == 0) return DVO_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *de, *dout;
+    int rc;
+    if ((rc = scratch(ctx, 24, (size_t)n * 8, &de)) || (rc = scratch(ctx, 25, (size_t)n * 4, &dout))) return rc;
+    HIP_TRY(hipMemcpy(de, ep, (size_t)n * 8, hipMemcpyHostToDevice));
+    HIP_TRY(launch_test_update_num_iters(p, (const double*)de, n, model_points, max_iters, (int32_t*)dout, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(out, dout, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double* models, int* n) {
+    if (!ctx || !q1 || !q2 || !models || !n) return DVO_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dq, *dm, *dn;
+    int rc;
+    if ((rc = scratch(ctx, 26, 20 * 8, &dq)) || (rc = scratch(ctx, 27, 90 * 8, &dm)) || (rc = scratch(ctx, 28, 8, &dn)))
+        return rc;
+    double q[20];
+    for (int i = 0; i < 5; ++i) {
+        q[4 * i] = q1[2 * i];
+        q[4 * i + 1] = q1[2 * i + 1];
+        q[4 * i + 2] = q2[2 * i];
+        q[4 * i + 3] = q2[2 * i + 1];
+    }
+    HIP_TRY(hipMemcpy(dq, q, sizeof(q), hipMemcpyHostToDevice));
+    HIP_TRY(launch_test_five_point((const double*)dq, (double*)dm, (int*)dn, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(n, dn, sizeof(int), hipMemcpyDeviceToHost));
+    if (*n > 0) HIP_TRY(hipMemcpy(models, dm, (size_t)*n * 72, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+}  // extern "C"

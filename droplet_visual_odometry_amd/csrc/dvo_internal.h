@@ -1,0 +1,146 @@
+// Internal declarations shared by the HIP translation units of libdvo_hip.so.
+//
+// Numerics contract: every file is compiled with
+// -ffp-contract=off and IEEE-correct f32/f64 division and sqrt, so each float
+// expression is evaluated in source order exactly like the CPU restatement of
+// OpenCV (no FMA contraction, round-to-nearest-even), which makes the device
+// results bit-identical to the oracle, not merely close.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dvo.h"
+
+namespace dvo {
+
+constexpr int kMaxLevels = 8;
+constexpr int kBandRows = 8;        // FAST band height (rows of output per workgroup)
+constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
+constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
+
+// Per-level geometry of one ORB plan (identical for every frame of a stream).
+struct LevelGeom {
+    int w, h;
+    float scale;          // getScale(l) = (float)pow(double(1.2f), l)
+    int nper;             // features per level
+    int64_t pyr_off;      // byte offset of level l (l >= 1) in a frame's pyramid slab
+    int64_t blur_off;     // byte offset of level l in a frame's blurred slab
+    int nbands;           // FAST bands over rows [31, h-31)
+    int band_base;        // first band index of this level within a frame
+    int band_cap;         // candidate capacity per band
+    int64_t band_cand_off;// u32 offset of this level's first band slot within a frame
+    int cand_cap;         // candidate capacity of the level (>= sum of its band caps)
+    int64_t cand_off;     // u32 offset of this level's gathered list within a frame
+    int tile_base;        // first blur tile of this level within a frame
+    int tiles_x, tiles_y; // blur tiling
+};
+
+struct Plan {
+    int w, h, nlevels, nfeatures, kp_cap, fast_threshold;
+    LevelGeom L[kMaxLevels];
+    int64_t pyr_stride;       // bytes per frame (levels 1..7)
+    int64_t blur_stride;      // bytes per frame (levels 0..7)
+    int total_bands;          // per frame
+    int64_t band_cand_stride; // u32 per frame
+    int64_t cand_stride;      // u32 per frame
+    int total_tiles;          // blur tiles per frame
+};
+
+// Device buffers of one stream (all sized for max_frames).
+struct Buffers {
+    uint8_t* pyr;
+    uint8_t* blur;
+    int32_t* band_cnt;
+    uint32_t* band_cand;
+    uint32_t* cand;       // gathered candidate keys (score<<24 | y<<12 | x)
+    float* resp;          // Harris responses parallel to cand
+    int32_t* sel_tmp;     // 2 * cand_stride per frame (Lpos / Rasc)
+    int32_t* cnt1;        // [F][8] after FAST retainBest
+    int32_t* cnt2;        // [F][8] after Harris retainBest
+    dvo_keypoint* kps;    // [F][kp_cap]
+    uint8_t* desc;        // [F][kp_cap][32]
+    int32_t* nkp;         // [F]
+    int32_t* nn;          // [2][F][kp_cap] packed (dist << 16 | idx), -1 none
+    int32_t* mq;          // [F][kp_cap] match queryIdx (sorted by (dist, q))
+    int32_t* mt;          // [F][kp_cap] match trainIdx
+    float* md;            // [F][kp_cap] match distance
+    int32_t* nmatch;      // [F]
+    float* pts;           // [F][kp_cap][4] (x1, y1, x2, y2) KeyPoint_convert pixel coords
+    double* npts;         // [F][kp_cap][4] normalised coords for RANSAC / recoverPose
+    double* models;       // [F][kChunk][10][9]
+    int32_t* status;      // [F] per-frame error flags
+    double* E;            // [F][90]
+    int32_t* info;        // [F][4] rows, inliers, iters, status
+    double* Rt;           // [F][12]
+    int32_t* good;        // [F]
+};
+
+constexpr int kChunk = 256;   // RANSAC iterations evaluated per round (one per thread)
+
+struct StreamParams {   // passed by value to every batch kernel
+    Plan plan;
+    Buffers buf;
+    const uint8_t* frames;
+    int64_t frame_stride;
+    int in_pitch;
+    int nframes;
+};
+
+__host__ __device__ inline const uint8_t* level_ptr(const StreamParams& P, int f, int l) {
+    return l == 0 ? P.frames + (int64_t)f * P.frame_stride : P.buf.pyr + (int64_t)f * P.plan.pyr_stride + P.plan.L[l].pyr_off;
+}
+__host__ __device__ inline int level_pitch(const StreamParams& P, int l) { return l == 0 ? P.in_pitch : P.plan.L[l].w; }
+__host__ __device__ inline uint8_t* blur_ptr(const StreamParams& P, int f, int l) {
+    return P.buf.blur + (int64_t)f * P.plan.blur_stride + P.plan.L[l].blur_off;
+}
+
+// ---- numerics helpers shared by device code ----------------------------------
+__device__ __forceinline__ int cv_round_f(float v) { return (int)__builtin_rintf(v); }
+__device__ __forceinline__ int cv_round_d(double v) { return (int)__builtin_rint(v); }
+__device__ __forceinline__ int cv_floor_d(double v) { int i = (int)v; return i - (i > v); }
+
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Arguments of the geometry kernels (findEssentialMat / recoverPose), shared by
+// the batched stream and the per-call C-ABI entry points.
+struct GeomArgs {
+    const float* pts_f;     // [pairs][pts_stride][4] pixel coords (x1, y1, x2, y2) or null
+    const double* pts_d;    // same layout in double, or null
+    const int32_t* m_arr;   // [pairs] correspondence counts (device) or null
+    int m_const;
+    int64_t pts_stride;
+    double fx, fy, cx, cy;
+    double prob, threshold;
+    int max_iters;
+    double dist_thresh;
+    double* npts;           // [pairs][pts_stride][4] normalised
+    double* models;         // [pairs][kChunk][10][9] scratch
+    double* E;              // [pairs][90]
+    int32_t* info;          // [pairs][4] rows, inliers, iters, status
+    uint8_t* mask;          // [pairs][pts_stride] findEssentialMat mask, or null
+    const uint8_t* mask_in; // [pairs][pts_stride] recoverPose input mask, or null
+    double* Rt;             // [pairs][12] R row-major then t
+    int32_t* good;          // [pairs]
+    int32_t* pick;          // [pairs] chosen decomposition 0..3, or null
+    uint8_t* pose_mask;     // [pairs][pts_stride][4] per-decomposition masks, or null
+};
+
+constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;
+
+// ---- host entry points of the kernels (implemented in the .hip files) -------
+hipError_t launch_orb(const StreamParams& P, hipStream_t s);
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s);
+hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s);
+hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
+hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
+hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
+                             dvo_dmatch* d_out, int* d_m, hipStream_t s);
+hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
+                                   int* d_k, hipStream_t s);
+hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int model_points, int max_iters,
+                                        int32_t* d_out, hipStream_t s);
+hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n, hipStream_t s);
+
+}  // namespace dvo

@@ -1,0 +1,1075 @@
+// Two-view geometry for gfx950: the MI355X replacement of
+//   cv.findEssentialMat(p_prev, p_cur, K, RANSAC, 0.999, 1.0)   visual_odometry_v3.py:297-300
+//   cv.recoverPose(E, p_prev, p_cur, K)                          visual_odometry_v3.py:303-306
+//   cv.triangulatePoints(P_prev, P_cur, c_prev.T, c_cur.T)       visual_odometry_v3.py:265
+//
+// ransac_kernel: one workgroup (256 threads) per frame pair.  RANSAC is
+// evaluated in rounds of up to kChunk iterations: thread 0 draws the round's
+// 5-point samples from cv::RNG((uint64)-1) exactly as getSubset does; every
+// thread then solves one sample with the 5-point kernel (Jacobi SVD + RNG
+// null-space completion, Nister coefficient matrix, LU solve, 10th-degree
+// polynomial, Durand-Kerner, per-root 3x3 SVD); the waves score all models'
+// Sampson errors over every correspondence (ballot popcounts); thread 0 then
+// replays RANSACPointSetRegistrator::run's sequential best/niters logic over
+// the round in iteration order, stopping where OpenCV would.  The result is
+// identical to the sequential loop; only iterations past OpenCV's stop are
+// wasted.
+// recover_pose_kernel: one workgroup per pair; thread 0 decomposes E, all
+// threads triangulate (4 poses x M points, one 4x4 Jacobi SVD per item).
+//
+// Every double expression mirrors oracle/geometry.cpp operation for operation
+// (compiled with -ffp-contract=off), so E, R and t are bit-identical to it.
+#include "dvo_internal.h"
+
+#include <cfloat>
+
+namespace dvo {
+
+struct Cx {
+    double re, im;
+};
+__device__ __forceinline__ Cx cmul(Cx a, Cx b) { return Cx{a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ Cx cadd(Cx a, Cx b) { return Cx{a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ Cx csub(Cx a, Cx b) { return Cx{a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ Cx cdiv(Cx a, Cx b) {
+    double t = 1. / (b.re * b.re + b.im * b.im);
+    return Cx{(a.re * b.re + a.im * b.im) * t, (-a.re * b.im + a.im * b.re) * t};
+}
+__device__ __forceinline__ double cabs_(Cx a) { return sqrt(a.re * a.re + a.im * a.im); }
+
+struct Rng {  // cv::RNG multiply-with-carry
+    uint64_t state;
+    __device__ unsigned next() {
+        state = (uint64_t)(unsigned)state * 4164903690U + (unsigned)(state >> 32);
+        return (unsigned)state;
+    }
+};
+
+__device__ __forceinline__ double dvo_hypot(double a, double b) {
+    a = fabs(a);
+    b = fabs(b);
+    if (a < b) {
+        double t = a;
+        a = b;
+        b = t;
+    }
+    if (a == 0) return b;
+    double r = b / a;
+    return a * sqrt(1.0 + r * r);
+}
+
+// lapack.cpp JacobiSVDImpl_ (see oracle/geometry.cpp jacobi_svd); compile-time
+// sizes keep every array in registers.  At has R >= max(N, N1) rows of M.
+template <int M, int N, int N1, int R>
+__device__ void jacobi_svd(double (&At)[R][M], double (&Wout)[N], double (&Vt)[N][N]) {
+    const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
+    double W[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            double t = At[i][k];
+            sd += t * t;
+        }
+        W[i] = sd;
+#pragma unroll
+        for (int k = 0; k < N; ++k) Vt[i][k] = 0;
+        Vt[i][i] = 1;
+    }
+    constexpr int max_iter = M > 30 ? M : 30;
+    for (int iter = 0; iter < max_iter; ++iter) {
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < N - 1; ++i)
+#pragma unroll
+            for (int j = i + 1; j < N; ++j) {
+                double a = W[i], p = 0, b = W[j];
+#pragma unroll
+                for (int k = 0; k < M; ++k) p += At[i][k] * At[j][k];
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
+                p *= 2;
+                double beta = a - b, gamma = dvo_hypot(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    double t0 = c * At[i][k] + s * At[j][k];
+                    double t1 = -s * At[i][k] + c * At[j][k];
+                    At[i][k] = t0;
+                    At[j][k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = true;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    double t0 = c * Vt[i][k] + s * Vt[j][k];
+                    double t1 = -s * Vt[i][k] + c * Vt[j][k];
+                    Vt[i][k] = t0;
+                    Vt[j][k] = t1;
+                }
+            }
+        if (!changed) break;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) {
+            double t = At[i][k];
+            sd += t * t;
+        }
+        W[i] = sqrt(sd);
+    }
+#pragma unroll
+    for (int i = 0; i < N - 1; ++i) {
+        int j = i;
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k)
+            if (wj < W[k]) {
+                j = k;
+                wj = W[k];
+            }
+#pragma unroll
+        for (int kk = i + 1; kk < N; ++kk)
+            if (j == kk) {
+                double t = W[i];
+                W[i] = W[kk];
+                W[kk] = t;
+#pragma unroll
+                for (int k = 0; k < M; ++k) {
+                    double u = At[i][k];
+                    At[i][k] = At[kk][k];
+                    At[kk][k] = u;
+                }
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    double u = Vt[i][k];
+                    Vt[i][k] = Vt[kk][k];
+                    Vt[kk][k] = u;
+                }
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) Wout[i] = W[i];
+    if (N1 == 0) return;
+    Rng rng{0x12345678ull};
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+        double sd = i < N ? W[i < N ? i : 0] : 0;
+        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
+            const double val0 = 1. / M;
+#pragma unroll
+            for (int k = 0; k < M; ++k) At[i][k] = (rng.next() & 256) != 0 ? val0 : -val0;
+            for (int it = 0; it < 2; it++)
+#pragma unroll
+                for (int j = 0; j < i; j++) {
+                    sd = 0;
+#pragma unroll
+                    for (int k = 0; k < M; ++k) sd += At[i][k] * At[j][k];
+                    double asum = 0;
+#pragma unroll
+                    for (int k = 0; k < M; ++k) {
+                        double t = At[i][k] - sd * At[j][k];
+                        At[i][k] = t;
+                        asum += fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+#pragma unroll
+                    for (int k = 0; k < M; ++k) At[i][k] *= asum;
+                }
+            sd = 0;
+#pragma unroll
+            for (int k = 0; k < M; ++k) {
+                double t = At[i][k];
+                sd += t * t;
+            }
+            sd = sqrt(sd);
+        }
+        double s = sd > minval ? 1 / sd : 0.;
+#pragma unroll
+        for (int k = 0; k < M; ++k) At[i][k] *= s;
+    }
+}
+
+// ---- Nister coefficient matrix (index tables = oracle PolyTables) ----------
+__device__ constexpr int kLL2Q[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
+__device__ constexpr int kQL2C[10][4] = {{0, 2, 4, 5},   {2, 3, 8, 9},    {4, 8, 10, 11},  {5, 9, 11, 12},
+                                         {3, 1, 6, 7},   {8, 6, 13, 14},  {9, 7, 14, 15},  {10, 13, 16, 17},
+                                         {11, 14, 17, 18}, {12, 15, 18, 19}};
+
+__device__ __forceinline__ void mul_ll(const double* a, const double* b, double* q) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) q[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] += a[i] * b[j];
+}
+__device__ __forceinline__ void mul_ql(const double* q, const double* l, double* c) {
+#pragma unroll
+    for (int k = 0; k < 20; ++k) c[k] = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += q[i] * l[j];
+}
+
+// Rows: the nine entries of 2 EE^T E - tr(EE^T) E (row-major), then det E;
+// columns 0..9 go to L (the matrix OpenCV inverts), 10..19 to G (its RHS).
+__device__ void coeff_matrix(const double (&EE)[4][9], double* L, double* G) {
+    double E[9][4];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+        E[e][0] = EE[0][e];
+        E[e][1] = EE[1][e];
+        E[e][2] = EE[2][e];
+        E[e][3] = EE[3][e];
+    }
+    double EEt[9][10], t1[10], t2[10];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double* o = EEt[i * 3 + j];
+            mul_ll(E[i * 3 + 0], E[j * 3 + 0], o);
+            mul_ll(E[i * 3 + 1], E[j * 3 + 1], t1);
+#pragma unroll
+            for (int k = 0; k < 10; ++k) o[k] = o[k] + t1[k];
+            mul_ll(E[i * 3 + 2], E[j * 3 + 2], t1);
+#pragma unroll
+            for (int k = 0; k < 10; ++k) o[k] = o[k] + t1[k];
+        }
+    double tr[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) tr[k] = (EEt[0][k] + EEt[4][k]) + EEt[8][k];
+    double row[20], c1[20], c2[20];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            mul_ql(EEt[i * 3 + 0], E[0 * 3 + j], row);
+            mul_ql(EEt[i * 3 + 1], E[1 * 3 + j], c1);
+#pragma unroll
+            for (int k = 0; k < 20; ++k) row[k] = row[k] + c1[k];
+            mul_ql(EEt[i * 3 + 2], E[2 * 3 + j], c1);
+#pragma unroll
+            for (int k = 0; k < 20; ++k) row[k] = row[k] + c1[k];
+            mul_ql(tr, E[i * 3 + j], c1);
+            const int r = i * 3 + j;
+#pragma unroll
+            for (int k = 0; k < 10; ++k) L[r * 10 + k] = 2.0 * row[k] - c1[k];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) G[r * 10 + k] = 2.0 * row[10 + k] - c1[10 + k];
+        }
+    mul_ll(E[4], E[8], t1);
+    mul_ll(E[5], E[7], t2);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
+    mul_ql(t1, E[0], row);
+    mul_ll(E[3], E[8], t1);
+    mul_ll(E[5], E[6], t2);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
+    mul_ql(t1, E[1], c1);
+    mul_ll(E[3], E[7], t1);
+    mul_ll(E[4], E[6], t2);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
+    mul_ql(t1, E[2], c2);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L[90 + k] = (row[k] - c1[k]) + c2[k];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) G[90 + k] = (row[10 + k] - c1[10 + k]) + c2[10 + k];
+}
+
+// LUImpl<double>(A, 10, b, 10, DBL_EPSILON*100) with dynamic pivoting (scratch).
+__device__ int lu_solve10(double* A, double* b) {
+    const double eps = DBL_EPSILON * 100;
+    const int m = 10, n = 10;
+    int p = 1;
+    for (int i = 0; i < m; i++) {
+        int k = i;
+        for (int j = i + 1; j < m; j++)
+            if (fabs(A[j * m + i]) > fabs(A[k * m + i])) k = j;
+        if (fabs(A[k * m + i]) < eps) return 0;
+        if (k != i) {
+            for (int j = i; j < m; j++) {
+                double t = A[i * m + j];
+                A[i * m + j] = A[k * m + j];
+                A[k * m + j] = t;
+            }
+            for (int j = 0; j < n; j++) {
+                double t = b[i * n + j];
+                b[i * n + j] = b[k * n + j];
+                b[k * n + j] = t;
+            }
+            p = -p;
+        }
+        double d = -1 / A[i * m + i];
+        for (int j = i + 1; j < m; j++) {
+            double alpha = A[j * m + i] * d;
+            for (int c = i + 1; c < m; c++) A[j * m + c] += alpha * A[i * m + c];
+            for (int c = 0; c < n; c++) b[j * n + c] += alpha * b[i * n + c];
+        }
+    }
+    for (int i = m - 1; i >= 0; i--)
+        for (int j = 0; j < n; j++) {
+            double s = b[i * n + j];
+            for (int k = i + 1; k < m; k++) s -= A[i * m + k] * b[k * n + j];
+            b[i * n + j] = s / A[i * m + i];
+        }
+    return p;
+}
+
+__device__ int solve_cubic(const double* c, double* x) {
+    double a0 = c[0], a1 = c[1], a2 = c[2], a3 = c[3];
+    double x0 = 0, x1 = 0, x2 = 0;
+    int n;
+    if (a0 == 0) {
+        if (a1 == 0) {
+            if (a2 == 0) n = a3 == 0 ? -1 : 0;
+            else {
+                x0 = -a3 / a2;
+                n = 1;
+            }
+        } else {
+            double d = a2 * a2 - 4 * a1 * a3;
+            if (d >= 0) {
+                d = sqrt(d);
+                double q1 = (-a2 + d) * 0.5, q2 = (a2 + d) * -0.5;
+                if (fabs(q1) > fabs(q2)) {
+                    x0 = q1 / a1;
+                    x1 = a3 / q1;
+                } else {
+                    x0 = q2 / a1;
+                    x1 = a3 / q2;
+                }
+                n = d > 0 ? 2 : 1;
+            } else
+                n = 0;
+        }
+    } else {
+        a0 = 1. / a0;
+        a1 *= a0;
+        a2 *= a0;
+        a3 *= a0;
+        double Q = (a1 * a1 - 3 * a2) * (1. / 9);
+        double R = (2 * a1 * a1 * a1 - 9 * a1 * a2 + 27 * a3) * (1. / 54);
+        double Qcubed = Q * Q * Q;
+        double d = Qcubed - R * R;
+        if (d > 0) {
+            double theta = acos(R / sqrt(Qcubed));
+            double sqrtQ = sqrt(Q);
+            double t0 = -2 * sqrtQ, t1 = theta * (1. / 3), t2 = a1 * (1. / 3);
+            x0 = t0 * cos(t1) - t2;
+            x1 = t0 * cos(t1 + (2. * M_PI / 3)) - t2;
+            x2 = t0 * cos(t1 + (4. * M_PI / 3)) - t2;
+            n = 3;
+        } else if (d == 0) {
+            if (R >= 0) {
+                x0 = -2 * pow(R, 1. / 3) - a1 / 3;
+                x1 = pow(R, 1. / 3) - a1 / 3;
+            } else {
+                x0 = 2 * pow(-R, 1. / 3) - a1 / 3;
+                x1 = -pow(-R, 1. / 3) - a1 / 3;
+            }
+            x2 = 0;
+            n = x0 == x1 ? 1 : 2;
+            x1 = x0 == x1 ? 0 : x1;
+        } else {
+            d = sqrt(-d);
+            double e = pow(d + fabs(R), 1. / 3);
+            if (R > 0) e = -e;
+            x0 = (e + Q / e) - a1 * (1. / 3);
+            n = 1;
+        }
+    }
+    x[0] = x0;
+    x[1] = x1;
+    x[2] = x2;
+    return n;
+}
+
+__device__ Cx same_root_step(Cx num, int num_same_root) {
+    double ore = num.re, oim = num.im;
+    int sq_times = num_same_root % 2 == 0 ? num_same_root / 2 : num_same_root / 2 - 1;
+    for (int j = 0; j < sq_times; j++) {
+        num.re = ore * ore + oim * oim;
+        num.re = sqrt(num.re);
+        num.re += ore;
+        num.im = num.re - ore;
+        num.re /= 2;
+        num.re = sqrt(num.re);
+        num.im /= 2;
+        num.im = sqrt(num.im);
+        if (ore < 0) num.im = -num.im;
+    }
+    if (num_same_root % 2 != 0) {
+        double cc[4], cr[3];
+        cc[3] = -(pow(ore, 3));
+        cc[2] = -(15 * pow(ore, 2) + 27 * pow(oim, 2));
+        cc[1] = -48 * ore;
+        cc[0] = 64;
+        solve_cubic(cc, cr);
+        if (cr[0] >= 0) num.re = pow(cr[0], 1. / 3);
+        else num.re = -pow(-cr[0], 1. / 3);
+        num.im = sqrt(pow(num.re, 2) / 3 - ore / (3 * num.re));
+    }
+    return num;
+}
+
+// solvePoly, full degree 10: constant indices keep roots/coeffs in registers.
+__device__ void solve_poly10(const double (&rc)[11], Cx (&roots)[10]) {
+    Cx coeffs[11];
+#pragma unroll
+    for (int i = 0; i <= 10; i++) coeffs[i] = Cx{rc[i], 0};
+    Cx p{1, 0}, r{1, 1};
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        roots[i] = p;
+        p = cmul(p, r);
+    }
+    for (int iter = 0; iter < 300; iter++) {
+        double maxDiff = 0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            p = roots[i];
+            Cx num = coeffs[10], denom = coeffs[10];
+            int num_same_root = 1;
+#pragma unroll
+            for (int j = 0; j < 10; j++) {
+                num = cadd(cmul(num, p), coeffs[10 - j - 1]);
+                if (j != i) {
+                    Cx d = csub(p, roots[j]);
+                    if (d.re == 0 && d.im == 0) num_same_root++;
+                    else denom = cmul(denom, d);
+                }
+            }
+            num = cdiv(num, denom);
+            if (num_same_root > 1) num = same_root_step(num, num_same_root);
+            roots[i] = csub(p, num);
+            const double an = cabs_(num);
+            maxDiff = maxDiff < an ? an : maxDiff;  // std::max(maxDiff, cv::abs(num))
+        }
+        if (maxDiff <= 0) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+        if (fabs(roots[i].im) < 1e-100) roots[i].im = 0;
+}
+
+// solvePoly generic (leading coefficients trimmed; rare): scratch arrays.
+__device__ int solve_poly_generic(const double* rc, int n0, Cx* roots) {
+    Cx coeffs[11];
+    for (int i = 0; i <= n0; i++) coeffs[i] = Cx{rc[i], 0};
+    int n = n0;
+    for (; n > 1; n--)
+        if (fabs(coeffs[n].re) + fabs(coeffs[n].im) > DBL_EPSILON) break;
+    Cx p{1, 0}, r{1, 1};
+    for (int i = 0; i < n; i++) {
+        roots[i] = p;
+        p = cmul(p, r);
+    }
+    for (int iter = 0; iter < 300; iter++) {
+        double maxDiff = 0;
+        for (int i = 0; i < n; i++) {
+            p = roots[i];
+            Cx num = coeffs[n], denom = coeffs[n];
+            int num_same_root = 1;
+            for (int j = 0; j < n; j++) {
+                num = cadd(cmul(num, p), coeffs[n - j - 1]);
+                if (j != i) {
+                    Cx d = csub(p, roots[j]);
+                    if (d.re == 0 && d.im == 0) num_same_root++;
+                    else denom = cmul(denom, d);
+                }
+            }
+            num = cdiv(num, denom);
+            if (num_same_root > 1) num = same_root_step(num, num_same_root);
+            roots[i] = csub(p, num);
+            double an = cabs_(num);
+            maxDiff = maxDiff < an ? an : maxDiff;
+        }
+        if (maxDiff <= 0) break;
+    }
+    for (int i = 0; i < n; i++)
+        if (fabs(roots[i].im) < 1e-100) roots[i].im = 0;
+    return n;
+}
+
+__device__ void poly_mul(const double* a, int na, const double* b, int nb, double* r) {
+#pragma unroll
+    for (int k = 0; k < na + nb - 1; ++k) r[k] = 0;
+#pragma unroll
+    for (int i = 0; i < na; ++i)
+#pragma unroll
+        for (int j = 0; j < nb; ++j) r[i + j] += a[i] * b[j];
+}
+
+// five-point.cpp EMEstimatorCallback::runKernel; q: 5 x (x1, y1, x2, y2)
+// normalised.  Writes up to 10 models (9 doubles each) and returns the count.
+__device__ int five_point(const double (&q)[5][4], double* models) {
+    double At[9][9], W[5], Vt[5][5];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) At[i][k] = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        double x1 = q[i][0], y1 = q[i][1], x2 = q[i][2], y2 = q[i][3];
+        At[i][0] = x1 * x2;
+        At[i][1] = y1 * x2;
+        At[i][2] = x2 + 0.0;
+        At[i][3] = x1 * y2;
+        At[i][4] = y1 * y2;
+        At[i][5] = y2 + 0.0;
+        At[i][6] = x1 + 0.0;
+        At[i][7] = y1 + 0.0;
+        At[i][8] = 1.0;
+    }
+    jacobi_svd<9, 5, 9, 9>(At, W, Vt);
+    double EE[4][9];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) EE[r][k] = At[5 + r][k] + 0.0;
+    double b[3 * 13];
+    {
+        // A = A.colRange(0,10).inv() * A.colRange(10,20) == solve(A1, A2, DECOMP_LU)
+        double L[100], G[100];
+        coeff_matrix(EE, L, G);
+        if (!lu_solve10(L, G))
+            for (int k = 0; k < 100; ++k) G[k] = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const double* a1 = G + (i * 2 + 4) * 10;
+            const double* a2 = G + (i * 2 + 5) * 10;
+            double row1[13], row2[13];
+#pragma unroll
+            for (int k = 0; k < 13; ++k) row1[k] = row2[k] = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) row1[1 + k] = (a1[k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) row1[5 + k] = (a1[3 + k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row1[9 + k] = (a1[6 + k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) row2[0 + k] = (a2[k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) row2[4 + k] = (a2[3 + k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row2[8 + k] = (a2[6 + k] + 0.0) + 0.0;
+#pragma unroll
+            for (int k = 0; k < 13; ++k) b[i * 13 + k] = row1[k] - row2[k];
+        }
+    }
+    double px[3][4], py[3][4], pc[3][5];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) px[j][k] = b[j * 13 + 3 - k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) py[j][k] = b[j * 13 + 7 - k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) pc[j][k] = b[j * 13 + 12 - k];
+    }
+    double u[8], v[8], m1[8], m2[8], m3[8], t1[11], t2[11], t3[11], c[11];
+    poly_mul(py[1], 4, pc[2], 5, u);
+    poly_mul(pc[1], 5, py[2], 4, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m1[k] = u[k] - v[k];
+    poly_mul(px[1], 4, pc[2], 5, u);
+    poly_mul(pc[1], 5, px[2], 4, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m2[k] = u[k] - v[k];
+    poly_mul(px[1], 4, py[2], 4, u);
+    poly_mul(py[1], 4, px[2], 4, v);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) m3[k] = u[k] - v[k];
+    poly_mul(px[0], 4, m1, 8, t1);
+    poly_mul(py[0], 4, m2, 8, t2);
+    poly_mul(pc[0], 5, m3, 7, t3);
+#pragma unroll
+    for (int k = 0; k < 11; ++k) c[k] = (t1[k] - t2[k]) + t3[k];
+
+    Cx roots[10];
+    int nr = 10;
+    if (fabs(c[10]) > DBL_EPSILON) {
+        solve_poly10(c, roots);
+    } else {
+        nr = solve_poly_generic(c, 10, roots);
+    }
+    int count = 0;
+    for (int i = 0; i < nr; ++i) {
+        if (fabs(roots[i].im) > 1e-10) continue;
+        double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+        double bz[3][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const double* br = b + j * 13;
+            bz[j][0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+            bz[j][1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+            bz[j][2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
+        }
+        double at3[3][3], w3[3], vt3[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) at3[r][k] = bz[k][r];
+        jacobi_svd<3, 3, 0, 3>(at3, w3, vt3);
+        if (fabs(vt3[2][2]) < 1e-10) continue;
+        double xs = vt3[2][0] / vt3[2][2], ys = vt3[2][1] / vt3[2][2];
+        double e[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) e[k] = (((EE[0][k] * xs + EE[1][k] * ys) + 0.0) + EE[2][k] * z1) + EE[3][k];
+        double s = 0;
+        s += e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3];
+        s += e[4] * e[4] + e[5] * e[5] + e[6] * e[6] + e[7] * e[7];
+        s += e[8] * e[8];
+        double inv_n = 1. / sqrt(s);
+        double* out = models + count * 9;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out[k] = e[k] * inv_n + 0.0;
+        count++;
+    }
+    return count;
+}
+
+__device__ __forceinline__ float sampson_err(const double* E, double x1, double y1, double x2, double y2) {
+    double ex0 = E[0] * x1 + E[1] * y1 + E[2] * 1.;
+    double ex1 = E[3] * x1 + E[4] * y1 + E[5] * 1.;
+    double ex2 = E[6] * x1 + E[7] * y1 + E[8] * 1.;
+    double et0 = E[0] * x2 + E[3] * y2 + E[6] * 1.;
+    double et1 = E[1] * x2 + E[4] * y2 + E[7] * 1.;
+    double x2tEx1 = x2 * ex0 + y2 * ex1 + 1. * ex2;
+    double a = ex0 * ex0, b = ex1 * ex1, c = et0 * et0, d = et1 * et1;
+    return (float)(x2tEx1 * x2tEx1 / (a + b + c + d));
+}
+
+__device__ int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
+    p = p > 0. ? p : 0.;
+    p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.;
+    ep = ep < 1. ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    double denom = 1. - pow(1. - ep, (double)model_points);
+    if (denom < DBL_MIN) return 0;
+    num = log(num);
+    denom = log(denom);
+    return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : cv_round_d(num / denom);
+}
+
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int pair_m(const GeomArgs& g, int p) { return g.m_arr ? g.m_arr[p] : g.m_const; }
+
+// findEssentialMat/recoverPose: col = (col - c)/f as OpenCV's MatExpr evaluates
+// it: col * (1/f) + (-c * (1/f)).
+__global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    const int m = pair_m(g, p);
+    const double ax = 1. / g.fx, ay = 1. / g.fy, bx = -g.cx * ax, by = -g.cy * ay;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < m; i += gridDim.x * 256) {
+        const int64_t o = ((int64_t)p * g.pts_stride + i) * 4;
+        double x1, y1, x2, y2;
+        if (g.pts_f) {
+            x1 = g.pts_f[o];
+            y1 = g.pts_f[o + 1];
+            x2 = g.pts_f[o + 2];
+            y2 = g.pts_f[o + 3];
+        } else {
+            x1 = g.pts_d[o];
+            y1 = g.pts_d[o + 1];
+            x2 = g.pts_d[o + 2];
+            y2 = g.pts_d[o + 3];
+        }
+        g.npts[o] = x1 * ax + bx;
+        g.npts[o + 1] = y1 * ay + by;
+        g.npts[o + 2] = x2 * ax + bx;
+        g.npts[o + 3] = y2 * ay + by;
+    }
+}
+
+constexpr int kRNT = 256;
+
+__global__ __launch_bounds__(kRNT) void ransac_kernel(GeomArgs g) {
+    const int p = blockIdx.x;
+    const int m = pair_m(g, p);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
+    double* E_out = g.E + (int64_t)p * 90;
+    int32_t* info = g.info + (int64_t)p * 4;
+    double* models = g.models + (int64_t)p * kChunk * 90;
+    __shared__ int s_idx[kChunk][5];
+    __shared__ int s_nmod[kChunk];
+    __shared__ int s_pref[kChunk + 1];
+    __shared__ int s_cnt[kChunk * 10];
+    __shared__ double s_best[9];
+    __shared__ uint64_t s_rng;
+    __shared__ int s_niters, s_iter, s_maxgood, s_done;
+    if (m < 5) {
+        if (tid == 0) {
+            info[0] = 0;
+            info[1] = 0;
+            info[2] = 0;
+            info[3] = DVO_EFEWPTS;
+        }
+        return;
+    }
+    const double thr = g.threshold / ((g.fx + g.fy) / 2);
+    const float t = (float)(thr * thr);
+    if (m == 5) {
+        if (tid == 0) {
+            double q[5][4];
+            for (int i = 0; i < 5; ++i)
+                for (int k = 0; k < 4; ++k) q[i][k] = npts[i * 4 + k];
+            int k = five_point(q, E_out);
+            info[0] = 3 * k;
+            info[1] = k > 0 ? 5 : 0;
+            info[2] = 1;
+            info[3] = k > 0 ? DVO_OK : DVO_ENOMODEL;
+            if (g.mask && k > 0)
+                for (int i = 0; i < 5; ++i) g.mask[(int64_t)p * g.pts_stride + i] = 1;
+        }
+        return;
+    }
+    if (tid == 0) {
+        s_rng = ~0ull;
+        s_niters = g.max_iters > 1 ? g.max_iters : 1;
+        s_iter = 0;
+        s_maxgood = 0;
+        s_done = 0;
+    }
+    __syncthreads();
+    while (true) {
+        const int iter0 = s_iter, niters0 = s_niters;
+        if (s_done || iter0 >= niters0) break;
+        const int C = min(kChunk, niters0 - iter0);
+        if (tid == 0) {  // getSubset for C consecutive iterations
+            Rng rng{s_rng};
+            for (int h = 0; h < C; ++h)
+                for (int i = 0; i < 5; ++i) {
+                    int v;
+                    for (;;) {
+                        v = (int)(rng.next() % (unsigned)m);
+                        int j;
+                        for (j = 0; j < i; ++j)
+                            if (s_idx[h][j] == v) break;
+                        if (j == i) break;
+                    }
+                    s_idx[h][i] = v;
+                }
+            s_rng = rng.state;
+        }
+        __syncthreads();
+        if (tid < C) {
+            double q[5][4];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const double* src = npts + (int64_t)s_idx[tid][i] * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[i][k] = src[k];
+            }
+            s_nmod[tid] = five_point(q, models + (int64_t)tid * 90);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int s = 0;
+            for (int h = 0; h < C; ++h) {
+                s_pref[h] = s;
+                s += s_nmod[h];
+            }
+            s_pref[C] = s;
+        }
+        __syncthreads();
+        // score every model of the round: one wave per model, lanes over points
+        const int T = s_pref[C];
+        for (int e = wid; e < T; e += kRNT / 64) {
+            int lo = 0, hi = C - 1;  // h with s_pref[h] <= e < s_pref[h+1]
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if (s_pref[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            const int h = lo, i = e - s_pref[h];
+            const double* Em = models + (int64_t)h * 90 + i * 9;
+            double Ed[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Ed[k] = Em[k];
+            int cnt = 0;
+            for (int j = lane; j < m; j += 64) {
+                const double* pt = npts + (int64_t)j * 4;
+                float err = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]);
+                cnt += __popcll(__ballot(err <= t));
+            }
+            if (lane == 0) s_cnt[h * 10 + i] = cnt;
+        }
+        __syncthreads();
+        if (tid == 0) {  // RANSACPointSetRegistrator::run, sequential replay
+            int niters = s_niters, maxgood = s_maxgood, it = iter0;
+            for (int h = 0; h < C; ++h, ++it) {
+                if (it >= niters) break;
+                for (int i = 0; i < s_nmod[h]; ++i) {
+                    int good = s_cnt[h * 10 + i];
+                    if (good > (maxgood > 4 ? maxgood : 4)) {
+                        const double* Em = models + (int64_t)h * 90 + i * 9;
+                        for (int k = 0; k < 9; ++k) s_best[k] = Em[k];
+                        maxgood = good;
+                        niters = ransac_update_num_iters(g.prob, (double)(m - good) / m, 5, niters);
+                    }
+                }
+            }
+            s_niters = niters;
+            s_maxgood = maxgood;
+            s_iter = it;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int maxgood = s_maxgood;
+        info[0] = maxgood > 0 ? 3 : 0;
+        info[1] = maxgood;
+        info[2] = s_iter;
+        info[3] = maxgood > 0 ? DVO_OK : DVO_ENOMODEL;
+        if (maxgood > 0)
+            for (int k = 0; k < 9; ++k) E_out[k] = s_best[k];
+    }
+    if (g.mask) {
+        __syncthreads();
+        if (s_maxgood > 0)
+            for (int j = tid; j < m; j += kRNT) {
+                const double* pt = npts + (int64_t)j * 4;
+                g.mask[(int64_t)p * g.pts_stride + j] = sampson_err(s_best, pt[0], pt[1], pt[2], pt[3]) <= t;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double det3(const double (&M)[3][3]) {
+    return M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+           M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+}
+
+__device__ __forceinline__ void matmul3(const double (&A)[3][3], const double (&B)[3][3], double (&C)[3][3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) C[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
+}
+
+// triangulate.cpp icvTriangulatePoints for one correspondence (P rows 3x4).
+__device__ __forceinline__ void triangulate_one(const double* P1, const double* P2, double x1, double y1, double x2,
+                                                double y2, double (&X)[4]) {
+    double A[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        A[0][k] = x1 * P1[8 + k] - P1[k];
+        A[1][k] = y1 * P1[8 + k] - P1[4 + k];
+        A[2][k] = x2 * P2[8 + k] - P2[k];
+        A[3][k] = y2 * P2[8 + k] - P2[4 + k];
+    }
+    double At[4][4], W[4], Vt[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) At[r][k] = A[k][r];
+    jacobi_svd<4, 4, 0, 4>(At, W, Vt);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) X[k] = Vt[3][k];
+}
+
+constexpr int kPNT = 256;
+
+__global__ __launch_bounds__(kPNT) void recover_pose_kernel(GeomArgs g) {
+    const int p = blockIdx.x;
+    const int m = pair_m(g, p);
+    const int tid = threadIdx.x;
+    __shared__ double sP[4][12];
+    __shared__ double sR[2][9];
+    __shared__ double st[3];
+    __shared__ int s_good[4];
+    __shared__ int s_ok;
+    const int32_t* info = g.info + (int64_t)p * 4;
+    if (tid == 0) {
+        s_ok = info[3] == DVO_OK && info[0] == 3;
+        for (int c = 0; c < 4; ++c) s_good[c] = 0;
+        if (s_ok) {
+            const double* E = g.E + (int64_t)p * 90;
+            double At[3][3], W[3], Vt[3][3], U[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) At[r][k] = E[k * 3 + r];
+            jacobi_svd<3, 3, 3, 3>(At, W, Vt);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) U[r][c] = At[c][r];
+            if (det3(U) < 0)
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) U[r][c] *= -1.;
+            if (det3(Vt) < 0)
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) Vt[r][c] *= -1.;
+            const double Wm[3][3] = {{0, 1, 0}, {-1, 0, 0}, {0, 0, 1}};
+            const double Wt[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+            double UW[3][3], R1[3][3], R2[3][3];
+            matmul3(U, Wm, UW);
+            matmul3(UW, Vt, R1);
+            matmul3(U, Wt, UW);
+            matmul3(UW, Vt, R2);
+            double tv[3];
+            for (int k = 0; k < 3; ++k) tv[k] = U[k][2] + 0.0;
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) {
+                    sR[0][r * 3 + k] = R1[r][k];
+                    sR[1][r * 3 + k] = R2[r][k];
+                }
+            for (int k = 0; k < 3; ++k) st[k] = tv[k];
+            for (int c = 0; c < 4; ++c) {
+                const double* Rs = sR[c & 1];
+                for (int r = 0; r < 3; ++r) {
+                    for (int k = 0; k < 3; ++k) sP[c][r * 4 + k] = Rs[r * 3 + k] + 0.0;
+                    sP[c][r * 4 + 3] = c < 2 ? tv[r] + 0.0 : 0.0 - tv[r];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (!s_ok) {
+        if (tid == 0) {
+            g.good[p] = 0;
+            if (g.pick) g.pick[p] = -1;
+        }
+        return;
+    }
+    const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
+    int cnt[4] = {0, 0, 0, 0};
+    for (int w = tid; w < 4 * m; w += kPNT) {
+        const int c = w & 3, i = w >> 2;
+        const double* pt = npts + (int64_t)i * 4;
+        double X[4];
+        triangulate_one(P0, sP[c], pt[0], pt[1], pt[2], pt[3], X);
+        bool ok = X[2] * X[3] > 0;
+        double q0 = X[0] / X[3], q1 = X[1] / X[3], q2 = X[2] / X[3], q3 = X[3] / X[3];
+        ok = (q2 < g.dist_thresh) && ok;
+        const double* Pr = sP[c] + 8;
+        double z = Pr[0] * q0 + Pr[1] * q1 + Pr[2] * q2 + Pr[3] * q3;
+        ok = (z > 0) && ok;
+        ok = (z < g.dist_thresh) && ok;
+        uint8_t mv = ok ? 255 : 0;
+        if (g.mask_in) mv &= g.mask_in[(int64_t)p * g.pts_stride + i];  // bitwise_and(mask, mask_c)
+        if (mv) cnt[c]++;
+        if (g.pose_mask) g.pose_mask[((int64_t)p * g.pts_stride + i) * 4 + c] = mv;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int v = cnt[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((tid & 63) == 0) atomicAdd(&s_good[c], v);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int* gd = s_good;
+        int pick;
+        if (gd[0] >= gd[1] && gd[0] >= gd[2] && gd[0] >= gd[3]) pick = 0;
+        else if (gd[1] >= gd[0] && gd[1] >= gd[2] && gd[1] >= gd[3]) pick = 1;
+        else if (gd[2] >= gd[0] && gd[2] >= gd[1] && gd[2] >= gd[3]) pick = 2;
+        else pick = 3;
+        double* Rt = g.Rt + (int64_t)p * 12;
+        for (int k = 0; k < 9; ++k) Rt[k] = sR[pick & 1][k];
+        for (int k = 0; k < 3; ++k) Rt[9 + k] = pick < 2 ? st[k] : 0.0 - st[k];
+        g.good[p] = gd[pick];
+        if (g.pick) g.pick[p] = pick;
+    }
+}
+
+__global__ void triangulate_kernel(const double* P, const double* x, int k, double* X) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= k) return;
+    double out[4];
+    triangulate_one(P, P + 12, x[i], x[k + i], x[2 * k + i], x[3 * k + i], out);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) X[r * k + i] = out[r];
+}
+
+__global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= P.nframes - 1) return;
+    dvo_pair_record r;
+    const int32_t* info = g.info + (int64_t)p * 4;
+    const double* E = g.E + (int64_t)p * 90;
+    const double* Rt = g.Rt + (int64_t)p * 12;
+    const bool ok = info[3] == DVO_OK && info[0] == 3;
+    for (int k = 0; k < 9; ++k) r.R[k] = ok ? Rt[k] : 0.0;
+    for (int k = 0; k < 3; ++k) r.t[k] = ok ? Rt[9 + k] : 0.0;
+    for (int k = 0; k < 9; ++k) r.E[k] = info[0] >= 3 ? E[k] : 0.0;
+    r.n_kp_prev = P.buf.nkp[p];
+    r.n_kp_cur = P.buf.nkp[p + 1];
+    r.n_matches = P.buf.nmatch[p];
+    r.n_inliers = info[1];
+    r.n_good = ok ? g.good[p] : 0;
+    r.ransac_iters = info[2];
+    r.status = (P.buf.status[p] | P.buf.status[p + 1]) ? DVO_ECAP : info[3];
+    r.n_models = info[0] / 3;
+    for (int k = 0; k < 7; ++k) r.reserved[k] = 0.0;
+    rec[p] = r;
+}
+
+__global__ void test_update_num_iters_kernel(double p, const double* ep, int n, int mp, int mi, int32_t* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = ransac_update_num_iters(p, ep[i], mp, mi);
+}
+
+__global__ void test_five_point_kernel(const double* qin, double* models, int* n) {
+    double q[5][4];
+    for (int i = 0; i < 5; ++i)
+        for (int k = 0; k < 4; ++k) q[i][k] = qin[i * 4 + k];
+    *n = five_point(q, models);
+}
+
+hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s) {
+    if (pairs <= 0) return hipSuccess;
+    if (stages & kStageNormalize) hipLaunchKernelGGL(normalize_kernel, dim3(4, pairs), dim3(256), 0, s, g);
+    if (stages & kStageRansac) hipLaunchKernelGGL(ransac_kernel, dim3(pairs), dim3(kRNT), 0, s, g);
+    if (stages & kStagePose) hipLaunchKernelGGL(recover_pose_kernel, dim3(pairs), dim3(kPNT), 0, s, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s) {
+    const int pairs = P.nframes - 1;
+    if (pairs <= 0) return hipSuccess;
+    hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac | kStagePose, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(records_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, P, g, records);
+    return hipGetLastError();
+}
+
+hipError_t launch_triangulate(const double* d_P, const double* d_x, int k, double* d_X, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    hipLaunchKernelGGL(triangulate_kernel, dim3((k + 255) / 256), dim3(256), 0, s, d_P, d_x, k, d_X);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int model_points, int max_iters,
+                                        int32_t* d_out, hipStream_t s) {
+    hipLaunchKernelGGL(test_update_num_iters_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, d_ep, n, model_points,
+                       max_iters, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n, hipStream_t s) {
+    hipLaunchKernelGGL(test_five_point_kernel, dim3(1), dim3(1), 0, s, d_q, d_models, d_n);
+    return hipGetLastError();
+}
+
+}  // namespace dvo

@@ -1,0 +1,266 @@
+// Brute-force Hamming matching for gfx950: the MI355X replacement of
+// cv::BFMatcher(NORM_HAMMING, crossCheck=True).match(prev_desc, cur_desc)
+// (scripts/visual_odometry_v3.py:75 and :219), followed by the reference's own
+// `sorted(matches, key=lambda x: x.distance)` (v3:221, a stable sort, so the
+// order is (distance, queryIdx)) and KeyPoint_convert of the matched keypoints
+// (v3:355, v3:358).
+//
+// nn_kernel: one workgroup = 512 queries x ALL trains.  The train descriptors
+// (<= kp_cap x 32 B) are staged once in LDS and read back as broadcast b128
+// loads; each thread keeps two query descriptors in registers and scans every
+// train with v_xor + v_bcnt (integer, 8 dwords), keeping a packed
+// (distance << 16 | index) minimum, which yields OpenCV's "first index at the
+// minimum distance" tie rule.  Forward (prev->cur) and backward (cur->prev)
+// directions run in the same launch (grid.y).
+// crosscheck_sort_kernel: mutual-NN filter, then a bitonic sort of the unique
+// keys (distance << 16 | queryIdx) in LDS, then the point gather.
+#include "dvo_internal.h"
+
+namespace dvo {
+namespace {
+
+constexpr int kNNThreads = 256;
+constexpr int kNNPerThread = 2;
+constexpr int kNNQ = kNNThreads * kNNPerThread;
+
+struct NNJob {
+    const uint8_t* q;
+    int nq;
+    const uint8_t* t;
+    int nt;
+    int32_t* out;
+};
+
+constexpr int kTrainChunk = 2048;   // trains staged per LDS fill (64 KB)
+
+__device__ __forceinline__ void nn_block(const NNJob& J, int qbase, uint4* lds) {
+    uint4 qa[kNNPerThread][2];
+    int best[kNNPerThread];
+    const uint4* qg = reinterpret_cast<const uint4*>(J.q);
+#pragma unroll
+    for (int r = 0; r < kNNPerThread; ++r) {
+        int q = qbase + r * kNNThreads + threadIdx.x;
+        best[r] = 0x7FFFFFFF;
+        if (q < J.nq) {
+            qa[r][0] = qg[2 * q];
+            qa[r][1] = qg[2 * q + 1];
+        } else {
+            qa[r][0] = make_uint4(0, 0, 0, 0);
+            qa[r][1] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    const uint4* tg = reinterpret_cast<const uint4*>(J.t);
+    for (int t0 = 0; t0 < J.nt; t0 += kTrainChunk) {
+        const int nc = min(kTrainChunk, J.nt - t0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nc * 2; i += kNNThreads) lds[i] = tg[2 * t0 + i];
+        __syncthreads();
+        for (int tt = 0; tt < nc; ++tt) {
+            const uint4 a = lds[2 * tt], b = lds[2 * tt + 1];
+            const int t = t0 + tt;
+#pragma unroll
+            for (int r = 0; r < kNNPerThread; ++r) {
+                int d = __popc(a.x ^ qa[r][0].x) + __popc(a.y ^ qa[r][0].y) + __popc(a.z ^ qa[r][0].z) +
+                        __popc(a.w ^ qa[r][0].w) + __popc(b.x ^ qa[r][1].x) + __popc(b.y ^ qa[r][1].y) +
+                        __popc(b.z ^ qa[r][1].z) + __popc(b.w ^ qa[r][1].w);
+                best[r] = min(best[r], (d << 16) | t);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kNNPerThread; ++r) {
+        int q = qbase + r * kNNThreads + threadIdx.x;
+        if (q < J.nq) J.out[q] = J.nt > 0 ? best[r] : -1;
+    }
+}
+
+__global__ __launch_bounds__(kNNThreads) void nn_stream_kernel(StreamParams P) {
+    extern __shared__ uint4 lds[];
+    const int p = blockIdx.z, dir = blockIdx.y;
+    const int fa = dir == 0 ? p : p + 1, fb = dir == 0 ? p + 1 : p;
+    NNJob J;
+    J.q = P.buf.desc + (int64_t)fa * P.plan.kp_cap * 32;
+    J.nq = min(P.buf.nkp[fa], P.plan.kp_cap);
+    J.t = P.buf.desc + (int64_t)fb * P.plan.kp_cap * 32;
+    J.nt = min(P.buf.nkp[fb], P.plan.kp_cap);
+    J.out = P.buf.nn + ((int64_t)dir * P.nframes + p) * P.plan.kp_cap;
+    const int qbase = blockIdx.x * kNNQ;
+    if (qbase >= J.nq) return;
+    nn_block(J, qbase, lds);
+}
+
+__global__ __launch_bounds__(kNNThreads) void nn_pair_kernel(const uint8_t* q, int nq, const uint8_t* t, int nt,
+                                                             int32_t* out) {
+    extern __shared__ uint4 lds[];
+    const int dir = blockIdx.y;
+    NNJob J{dir == 0 ? q : t, dir == 0 ? nq : nt, dir == 0 ? t : q, dir == 0 ? nt : nq, out + (dir == 0 ? 0 : nq)};
+    const int qbase = blockIdx.x * kNNQ;
+    if (qbase >= J.nq) return;
+    nn_block(J, qbase, lds);
+}
+
+constexpr int kXNT = 1024;
+constexpr int kMaxSort = 8192;
+
+// Mutual-NN / legacy cross check + stable (distance, queryIdx) order.
+// Writes m keys sorted ascending into keys[] (LDS) and returns m.
+__device__ int crosscheck_sort(const int32_t* fwd, const int32_t* bwd, int nq, int nt, int mode, uint32_t* keys,
+                               int* scan_lds) {
+    __shared__ int s_m;
+    if (threadIdx.x == 0) s_m = 0;
+    __syncthreads();
+    if (mode == 2) {
+        // OpenCV 3.x: for each train t (reverse NN q = bwd[t]), keep per query the
+        // train with the smallest distance, first t on ties.
+        for (int q = threadIdx.x; q < nq; q += kXNT) keys[q] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (int t = threadIdx.x; t < nt; t += kXNT) {
+            int b = bwd[t];
+            if (b < 0) continue;
+            int q = b & 0xFFFF, d = b >> 16;
+            atomicMin(&keys[q], ((uint32_t)d << 16) | (uint32_t)t);
+        }
+        __syncthreads();
+        // convert to (d << 16 | q) keys; the train index is recovered from bwd later
+        for (int q = threadIdx.x; q < nq; q += kXNT) {
+            uint32_t k = keys[q];
+            keys[kMaxSort + q] = k;  // stash (d << 16 | t) in the upper half
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < nq; q += kXNT) {
+            uint32_t k = keys[kMaxSort + q];
+            keys[q] = 0xFFFFFFFFu;
+            if (k != 0xFFFFFFFFu) {
+                int slot = atomicAdd(&s_m, 1);
+                keys[slot] = ((k >> 16) << 16) | (uint32_t)q;
+            }
+        }
+    } else {
+        for (int q = threadIdx.x; q < nq; q += kXNT) {
+            int f = fwd[q];
+            if (f < 0) continue;
+            int t = f & 0xFFFF;
+            if (mode == 1 && (bwd[t] & 0xFFFF) != q) continue;
+            int slot = atomicAdd(&s_m, 1);
+            keys[slot] = ((uint32_t)(f >> 16) << 16) | (uint32_t)q;
+        }
+    }
+    __syncthreads();
+    const int m = s_m;
+    int n2 = 1;
+    while (n2 < m) n2 <<= 1;
+    for (int i = m + threadIdx.x; i < n2; i += kXNT) keys[i] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += kXNT) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    uint32_t a = keys[i], b = keys[ixj];
+                    bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        keys[i] = b;
+                        keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    (void)scan_lds;
+    return m;
+}
+
+__global__ __launch_bounds__(kXNT) void crosscheck_stream_kernel(StreamParams P, int mode) {
+    __shared__ uint32_t keys[2 * kMaxSort];
+    __shared__ int scan_lds[32];
+    const int p = blockIdx.x;
+    const int cap = P.plan.kp_cap;
+    const int nq = min(P.buf.nkp[p], cap), nt = min(P.buf.nkp[p + 1], cap);
+    const int32_t* fwd = P.buf.nn + (int64_t)p * cap;
+    const int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
+    const int m = crosscheck_sort(fwd, bwd, nq, nt, mode, keys, scan_lds);
+    const dvo_keypoint* ka = P.buf.kps + (int64_t)p * cap;
+    const dvo_keypoint* kb = P.buf.kps + (int64_t)(p + 1) * cap;
+    int32_t* mq = P.buf.mq + (int64_t)p * cap;
+    int32_t* mt = P.buf.mt + (int64_t)p * cap;
+    float* md = P.buf.md + (int64_t)p * cap;
+    float* pts = P.buf.pts + (int64_t)p * cap * 4;
+    for (int i = threadIdx.x; i < m; i += kXNT) {
+        const uint32_t k = keys[i];
+        const int q = k & 0xFFFF;
+        const int t = mode == 2 ? (int)(keys[kMaxSort + q] & 0xFFFF) : (fwd[q] & 0xFFFF);
+        mq[i] = q;
+        mt[i] = t;
+        md[i] = (float)(k >> 16);
+        pts[4 * i + 0] = ka[q].x;
+        pts[4 * i + 1] = ka[q].y;
+        pts[4 * i + 2] = kb[t].x;
+        pts[4 * i + 3] = kb[t].y;
+    }
+    if (threadIdx.x == 0) P.buf.nmatch[p] = m;
+}
+
+// Single pair (C-ABI dvo_bf_match_hamming): output in queryIdx order like
+// OpenCV (the caller's Python applies the stable distance sort itself).
+__global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* nn, int nq, int nt, int mode,
+                                                               dvo_dmatch* out, int* m_out) {
+    __shared__ uint32_t keys[2 * kMaxSort];
+    __shared__ int scan_lds[32];
+    const int32_t* fwd = nn;
+    const int32_t* bwd = nn + nq;
+    const int m = crosscheck_sort(fwd, bwd, nq, nt, mode, keys, scan_lds);
+    // re-sort by queryIdx: keys are unique (d<<16|q); rewrite as (q<<16|d) and sort again
+    for (int i = threadIdx.x; i < m; i += kXNT) {
+        uint32_t k = keys[i];
+        keys[i] = ((k & 0xFFFF) << 16) | (k >> 16);
+    }
+    __syncthreads();
+    int n2 = 1;
+    while (n2 < m) n2 <<= 1;
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n2; i += kXNT) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    uint32_t a = keys[i], b = keys[ixj];
+                    bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        keys[i] = b;
+                        keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < m; i += kXNT) {
+        const uint32_t k = keys[i];
+        const int q = k >> 16, d = k & 0xFFFF;
+        const int t = mode == 2 ? (int)(keys[kMaxSort + q] & 0xFFFF) : (fwd[q] & 0xFFFF);
+        out[i] = dvo_dmatch{q, t, 0, (float)d};
+    }
+    if (threadIdx.x == 0) *m_out = m;
+}
+
+}  // namespace
+
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s) {
+    if (P.nframes < 2) return hipSuccess;
+    const int cap = P.plan.kp_cap;
+    const size_t lds = (size_t)(cap < kTrainChunk ? cap : kTrainChunk) * 32;
+    dim3 grid((cap + kNNQ - 1) / kNNQ, 2, P.nframes - 1);
+    hipLaunchKernelGGL(nn_stream_kernel, grid, dim3(kNNThreads), lds, s, P);
+    hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
+    return hipGetLastError();
+}
+
+hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
+                             dvo_dmatch* d_out, int* d_m, hipStream_t s) {
+    const int nmax = nq > nt ? nq : nt;
+    const size_t lds = (size_t)(nmax < kTrainChunk ? (nmax > 0 ? nmax : 1) : kTrainChunk) * 32;
+    dim3 grid((nmax + kNNQ - 1) / kNNQ, 2);
+    hipLaunchKernelGGL(nn_pair_kernel, grid, dim3(kNNThreads), lds, s, d_q, nq, d_t, nt, d_nn);
+    hipLaunchKernelGGL(crosscheck_pair_kernel, dim3(1), dim3(kXNT), 0, s, d_nn, nq, nt, cross_check, d_out, d_m);
+    return hipGetLastError();
+}
+
+}  // namespace dvo

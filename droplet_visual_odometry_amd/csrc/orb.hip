@@ -1,0 +1,776 @@
+// ORB detect-and-compute for gfx950: the MI355X replacement of
+// cv::ORB::detectAndCompute as called at scripts/visual_odometry_v3.py:373
+// (cv.ORB_create() defaults chosen at v3:96).  Batched: every launch covers all
+// frames of a stream batch (grid.y / grid.z = frame), so one batch of F frames
+// runs 7 resize launches + 6 detect/describe launches regardless of F.
+//
+// Stages (DESIGN.md §4 lists the roofline of each):
+//   resize_level_kernel   INTER_LINEAR_EXACT 8-bit fixed point, level l-1 -> l
+//   blur_kernel           GaussianBlur 7x7 sigma 2, 8-bit fixed-point separable
+//   fast_band_kernel      FAST-9/16 + strict 3x3 NMS + border cut + raster-ordered
+//                         compaction, one 8-row band of one level per workgroup
+//   select_fast_kernel    KeyPointsFilter::retainBest(2n) by FAST score: exact
+//                         emulation of libstdc++ nth_element + partition
+//   harris_kernel         HarrisResponses(blockSize 7, k 0.04)
+//   select_harris_kernel  retainBest(n) by Harris response
+//   describe_kernel       ICAngles + pt scaling + rBRIEF-256, one wave per keypoint
+#include "dvo_internal.h"
+
+#include <climits>
+
+namespace dvo {
+
+namespace {
+
+__constant__ int8_t c_pattern[256 * 4] = {
+#include "../../data/orb_bit_pattern_31.inc"
+};
+
+// ICAngles u_max for halfPatchSize 15 (orb.cpp computeKeyPoints): cvRound of
+// sqrt(225 - v^2) for v <= 11, then the symmetry fix-up; pinned by a test.
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
+// FAST 16-pixel Bresenham circle (dx, dy), fast.cpp makeOffsets.
+constexpr int kCdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+constexpr int kCdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+// ------------------------------------------------------------------------
+// Level l from level l-1: resize.cpp resize_bitExact<uchar, interpolationLinear>.
+struct LinCoef {
+    int ofs, c0, c1, mode;  // mode 0 interior, 1 left edge (src[0]), 2 right edge (src[last])
+};
+
+__device__ LinCoef lin_coef(int val, int srcsize, int dstsize) {
+    const double inv_scale = (double)dstsize / srcsize;
+    const double scale = 1.0 / inv_scale;
+    double fval = scale * ((double)val + 0.5) - 0.5;
+    int ival = cv_floor_d(fval);
+    LinCoef c{0, 0, 0, 0};
+    if (ival >= 0 && srcsize > 1) {
+        if (ival < srcsize - 1) {
+            c.ofs = ival;
+            c.c1 = cv_round_d((fval - (double)ival) * 256.0);
+            c.c0 = 256 > c.c1 ? 256 - c.c1 : 0;
+        } else {
+            c.ofs = srcsize - 1;
+            c.mode = 2;
+        }
+    } else {
+        c.mode = 1;
+    }
+    return c;
+}
+
+// OpenCV decides edges from the running min/max over all positions; since
+// fval is monotone in val, "left edge" = prefix with ival < 0 and "right edge"
+// = suffix with ival >= srcsize-1, which is what lin_coef's mode encodes.
+__device__ __forceinline__ uint32_t hline(const uint8_t* row, const LinCoef& cx, int sw) {
+    if (cx.mode == 1) return (uint32_t)row[0] << 8;
+    if (cx.mode == 2) return (uint32_t)row[sw - 1] << 8;
+    return (uint32_t)cx.c0 * row[cx.ofs] + (uint32_t)cx.c1 * row[cx.ofs + 1];
+}
+
+__global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l) {
+    const int f = blockIdx.z;
+    const LevelGeom& S = P.plan.L[l - 1];
+    const LevelGeom& D = P.plan.L[l];
+    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (dx >= D.w || dy >= D.h) return;
+    const uint8_t* src = level_ptr(P, f, l - 1);
+    const int sp = level_pitch(P, l - 1);
+    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
+    LinCoef cx = lin_coef(dx, S.w, D.w);
+    LinCoef cy = lin_coef(dy, S.h, D.h);
+    uint32_t v;
+    if (cy.mode != 0) {
+        const uint8_t* row = src + (int64_t)(cy.mode == 1 ? 0 : S.h - 1) * sp;
+        uint32_t hh = hline(row, cx, S.w);
+        v = (hh + 128) >> 8;
+    } else {
+        uint32_t h0 = hline(src + (int64_t)cy.ofs * sp, cx, S.w);
+        uint32_t h1 = hline(src + (int64_t)(cy.ofs + 1) * sp, cx, S.w);
+        v = (h0 * (uint32_t)cy.c0 + h1 * (uint32_t)cy.c1 + 32768u) >> 16;
+    }
+    dst[(int64_t)dy * D.w + dx] = (uint8_t)(v > 255 ? 255 : v);
+}
+
+// ------------------------------------------------------------------------
+// GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) with the 8-bit kernel
+// {18,34,49,55,49,34,18}: int row sums, (colsum + 2^15) >> 16.
+constexpr int kBTX = 64, kBTY = 16;
+__device__ __forceinline__ int refl101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+    return p;
+}
+
+__global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
+    const int f = blockIdx.y;
+    int item = blockIdx.x;
+    int l = 0;
+    while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].tile_base) ++l;
+    const LevelGeom& G = P.plan.L[l];
+    const int t = item - G.tile_base;
+    const int tx0 = (t % G.tiles_x) * kBTX, ty0 = (t / G.tiles_x) * kBTY;
+    const uint8_t* src = level_ptr(P, f, l);
+    const int sp = level_pitch(P, l);
+    uint8_t* dst = blur_ptr(P, f, l);
+    __shared__ uint8_t tile[kBTY + 6][kBTX + 6];
+    __shared__ int rows[kBTY + 6][kBTX];
+    for (int i = threadIdx.x; i < (kBTY + 6) * (kBTX + 6); i += 256) {
+        int ry = i / (kBTX + 6), rx = i % (kBTX + 6);
+        int y = refl101(ty0 + ry - 3, G.h), x = refl101(tx0 + rx - 3, G.w);
+        tile[ry][rx] = src[(int64_t)y * sp + x];
+    }
+    __syncthreads();
+    const int k[7] = {18, 34, 49, 55, 49, 34, 18};
+    for (int i = threadIdx.x; i < (kBTY + 6) * kBTX; i += 256) {
+        int ry = i / kBTX, rx = i % kBTX;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) s += k[j] * tile[ry][rx + j];
+        rows[ry][rx] = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBTY * kBTX; i += 256) {
+        int ry = i / kBTX, rx = i % kBTX;
+        int y = ty0 + ry, x = tx0 + rx;
+        if (y >= G.h || x >= G.w) continue;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) s += k[j] * rows[ry + j][rx];
+        int v = (s + (1 << 15)) >> 16;
+        dst[(int64_t)y * G.w + x] = (uint8_t)(v > 255 ? 255 : v);
+    }
+}
+
+// ------------------------------------------------------------------------
+// FAST-9/16 over one band of kBandRows output rows.
+constexpr int kFastNT = 256;
+
+__device__ __forceinline__ int fast_score16(const int* c, int v, int threshold) {
+    // fast.cpp cornerScore<16> (scalar form): d[k] = v - circle[k], k in [0, 25)
+    int d[25];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = v - c[k];
+#pragma unroll
+    for (int k = 16; k < 25; ++k) d[k] = d[k - 16];
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+__device__ __forceinline__ bool has_run9(uint32_t m) {
+    uint32_t m2 = m | (m << 16);
+    uint32_t a = m2 & (m2 >> 1);  // runs >= 2
+    a = a & (a >> 2);             // >= 4
+    a = a & (a >> 4);             // >= 8
+    a = a & (m2 >> 8);            // >= 9
+    return (a & 0xFFFFu) != 0;
+}
+
+__device__ __forceinline__ int block_excl_scan(int v, int& total, int* lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // inclusive scan within the wave
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        int c = lds[w];
+        if (w < wid) off += c;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return off + x - v;
+}
+
+__global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
+    const int f = blockIdx.y;
+    const int item = blockIdx.x;
+    int l = 0;
+    while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].band_base) ++l;
+    const LevelGeom& G = P.plan.L[l];
+    const int b = item - G.band_base;
+    const int w = G.w, h = G.h;
+    const int r0 = kBorder + b * kBandRows;
+    const int r1 = min(r0 + kBandRows, h - kBorder);
+    const int thr = P.plan.fast_threshold;
+    const uint8_t* src = level_ptr(P, f, l);
+    const int sp = level_pitch(P, l);
+    const int SW = ((w + 3) & ~3) + 16;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* img = smem;                       // 16 rows: y in [r0-4, r0+12)
+    uint8_t* sc = smem + 16 * SW;              // 10 rows: y in [r0-1, r0+9)
+    __shared__ int scan_lds[16];
+    const int ylo = r0 - 4, yhi = min(r0 + 12, h);
+    // load rows (bytes; rows are short and L2-resident)
+    for (int i = threadIdx.x; i < (yhi - ylo) * w; i += kFastNT) {
+        int ry = i / w, x = i - ry * w;
+        img[ry * SW + x] = src[(int64_t)(ylo + ry) * sp + x];
+    }
+    __syncthreads();
+    // scores for rows [r0-1, r1] (NMS neighbourhood), columns in groups of 4
+    const int gx0 = 28, gx1 = ((w - 28) + 3) & ~3;   // [28, ~w-28)
+    const int ngx = (gx1 - gx0) / 4;
+    const int nsr = r1 - r0 + 2;
+    for (int i = threadIdx.x; i < nsr * ngx; i += kFastNT) {
+        int sr = i / ngx, g = i - sr * ngx;
+        int y = r0 - 1 + sr;
+        int x0 = gx0 + 4 * g;
+        const uint8_t* base = img + (y - ylo) * SW;
+        uint32_t out = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int x = x0 + j;
+            int score = 0;
+            if (x >= 3 && x <= w - 4 && y >= 3 && y <= h - 4) {
+                int v = base[x];
+                int c[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) c[k] = base[kCdy[k] * SW + x + kCdx[k]];
+                uint32_t br = 0, dk = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    br |= (uint32_t)(c[k] > v + thr) << k;
+                    dk |= (uint32_t)(c[k] < v - thr) << k;
+                }
+                if (has_run9(br) || has_run9(dk)) score = fast_score16(c, v, thr);
+            }
+            out |= (uint32_t)(score & 0xFF) << (8 * j);
+        }
+        *reinterpret_cast<uint32_t*>(sc + sr * SW + x0) = out;
+    }
+    __syncthreads();
+    // NMS + raster-ordered compaction over rows [r0, r1), cols [31, w-31)
+    const int Wc = w - 2 * kBorder;
+    const int total = (r1 - r0) * Wc;
+    const int chunk = (total + kFastNT - 1) / kFastNT;
+    const int p0 = threadIdx.x * chunk, p1 = min(p0 + chunk, total);
+    auto keep = [&](int p, int& score, int& x, int& y) {
+        y = r0 + p / Wc;
+        x = kBorder + p % Wc;
+        const uint8_t* s = sc + (y - (r0 - 1)) * SW + x;
+        score = s[0];
+        return score > 0 && score > s[-1] && score > s[1] && score > s[-SW - 1] && score > s[-SW] &&
+               score > s[-SW + 1] && score > s[SW - 1] && score > s[SW] && score > s[SW + 1];
+    };
+    int cnt = 0;
+    for (int p = p0; p < p1; ++p) {
+        int s, x, y;
+        cnt += keep(p, s, x, y);
+    }
+    int tot;
+    int off = block_excl_scan(cnt, tot, scan_lds);
+    uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)b * G.band_cap;
+    for (int p = p0; p < p1; ++p) {
+        int s, x, y;
+        if (keep(p, s, x, y)) outp[off++] = ((uint32_t)s << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    }
+    if (threadIdx.x == 0) P.buf.band_cnt[(int64_t)f * P.plan.total_bands + item] = tot;
+}
+
+// ------------------------------------------------------------------------
+// KeyPointsFilter::retainBest — exact emulation of libstdc++'s introselect
+// (median-of-3 + unguarded Hoare partition, heap-select fallback, final
+// insertion sort) followed by the bidirectional std::partition.  Each Hoare
+// partition step is computed in parallel: the k-th left stop is the k-th
+// position (ascending) holding a value <= pivot, the k-th right stop the k-th
+// position (descending) holding a value >= pivot; pairs are swapped while
+// left < right, and the returned cut is min(L[k*], R[k*-1]).
+struct FastKeys {
+    uint32_t* key;
+    struct Elem {
+        uint32_t k;
+    };
+    __device__ int val(int i) const { return (int)(key[i] >> 24); }
+    __device__ void swap(int i, int j) const {
+        uint32_t t = key[i];
+        key[i] = key[j];
+        key[j] = t;
+    }
+    __device__ Elem get(int i) const { return Elem{key[i]}; }
+    __device__ void put(int i, Elem e) const { key[i] = e.k; }
+    __device__ static int ev(Elem e) { return (int)(e.k >> 24); }
+};
+
+struct HarrisVals {
+    float* v;
+    uint32_t* key;
+    struct Elem {
+        float v;
+        uint32_t k;
+    };
+    __device__ float val(int i) const { return v[i]; }
+    __device__ void swap(int i, int j) const {
+        float t = v[i];
+        v[i] = v[j];
+        v[j] = t;
+        uint32_t u = key[i];
+        key[i] = key[j];
+        key[j] = u;
+    }
+    __device__ Elem get(int i) const { return Elem{v[i], key[i]}; }
+    __device__ void put(int i, Elem e) const {
+        v[i] = e.v;
+        key[i] = e.k;
+    }
+    __device__ static float ev(Elem e) { return e.v; }
+};
+
+__device__ __forceinline__ void block_excl_scan2(int fa, int fb, int& pa, int& pb, int& ta, int& tb, int* lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    unsigned long long ma = __ballot(fa), mb = __ballot(fb);
+    unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    if (lane == 0) {
+        lds[wid] = __popcll(ma);
+        lds[32 + wid] = __popcll(mb);
+    }
+    __syncthreads();
+    int oa = 0, ob = 0, sa = 0, sb = 0;
+    for (int w = 0; w < nw; ++w) {
+        int ca = lds[w], cb = lds[32 + w];
+        if (w < wid) {
+            oa += ca;
+            ob += cb;
+        }
+        sa += ca;
+        sb += cb;
+    }
+    __syncthreads();
+    pa = oa + __popcll(ma & lt);
+    pb = ob + __popcll(mb & lt);
+    ta = sa;
+    tb = sb;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) lds[wid] = v;
+    __syncthreads();
+    int s = 0;
+    for (int w = 0; w < nw; ++w) s += lds[w];
+    __syncthreads();
+    return s;
+}
+
+template <class A, class V>
+__device__ int partition_step(const A& a, int first, int last, V p, int32_t* Lpos, int32_t* Rasc, int* lds) {
+    int nL = 0, nR = 0;
+    for (int base = first; base < last; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool in = i < last;
+        V v = in ? a.val(i) : p;
+        int fl = in && i >= first + 1 && !(v > p);
+        int fr = in && !(p > v);
+        int pa, pb, ta, tb;
+        block_excl_scan2(fl, fr, pa, pb, ta, tb, lds);
+        if (fl) Lpos[nL + pa] = i;
+        if (fr) Rasc[nR + pb] = i;
+        nL += ta;
+        nR += tb;
+    }
+    __syncthreads();
+    const int K = min(nL, nR);
+    int cnt = 0;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) cnt += Lpos[k] < Rasc[nR - 1 - k];
+    const int kstar = block_sum(cnt, lds);
+    for (int k = threadIdx.x; k < kstar; k += blockDim.x) a.swap(Lpos[k], Rasc[nR - 1 - k]);
+    const int cl = kstar < nL ? Lpos[kstar] : INT_MAX;
+    const int cr = kstar > 0 ? Rasc[nR - kstar] : INT_MAX;
+    __syncthreads();
+    return min(cl, cr);
+}
+
+// libstdc++ heap primitives, single thread (rare depth-limit fallback).
+template <class A>
+__device__ void adjust_heap(const A& a, int first, int hole, int len, typename A::Elem value) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (a.val(first + second) > a.val(first + second - 1)) second--;
+        a.put(first + hole, a.get(first + second));
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        a.put(first + hole, a.get(first + second - 1));
+        hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && a.val(first + parent) > A::ev(value)) {
+        a.put(first + hole, a.get(first + parent));
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a.put(first + hole, value);
+}
+
+template <class A>
+__device__ void heap_select(const A& a, int first, int middle, int last) {
+    const int len = middle - first;
+    if (len >= 2) {
+        int parent = (len - 2) / 2;
+        while (true) {
+            adjust_heap(a, first, parent, len, a.get(first + parent));
+            if (parent == 0) break;
+            parent--;
+        }
+    }
+    for (int i = middle; i < last; ++i)
+        if (a.val(i) > a.val(first)) {
+            typename A::Elem v = a.get(i);
+            a.put(i, a.get(first));
+            adjust_heap(a, first, 0, len, v);
+        }
+}
+
+template <class A>
+__device__ void insertion_sort(const A& a, int first, int last) {
+    if (first == last) return;
+    for (int i = first + 1; i != last; ++i) {
+        typename A::Elem v = a.get(i);
+        if (A::ev(v) > a.val(first)) {
+            for (int k = i; k > first; --k) a.put(k, a.get(k - 1));
+            a.put(first, v);
+        } else {
+            int k = i;
+            while (A::ev(v) > a.val(k - 1)) {
+                a.put(k, a.get(k - 1));
+                --k;
+            }
+            a.put(k, v);
+        }
+    }
+}
+
+template <class A>
+__device__ void move_median_to_first(const A& a, int result, int x, int y, int z) {
+    if (a.val(x) > a.val(y)) {
+        if (a.val(y) > a.val(z)) a.swap(result, y);
+        else if (a.val(x) > a.val(z)) a.swap(result, z);
+        else a.swap(result, x);
+    } else if (a.val(x) > a.val(z)) a.swap(result, x);
+    else if (a.val(y) > a.val(z)) a.swap(result, z);
+    else a.swap(result, y);
+}
+
+// Returns the retained size; the first `result` entries hold the kept
+// elements in libstdc++ order.  Must be called by the whole block.
+template <class A>
+__device__ int retain_best_block(const A& a, int n, int npoints, int depth, int32_t* Lpos, int32_t* Rasc, int* lds) {
+    if (npoints < 0 || n <= npoints) return n;
+    if (npoints == 0) return 0;
+    const int nth = npoints - 1;
+    int first = 0, last = n;
+    if (depth < 0) depth = 2 * (31 - __clz(n));
+    bool heap_done = false;
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (threadIdx.x == 0) {
+                heap_select(a, first, nth + 1, last);
+                a.swap(first, nth);
+            }
+            heap_done = true;
+            break;
+        }
+        --depth;
+        if (threadIdx.x == 0) move_median_to_first(a, first, first + 1, first + (last - first) / 2, last - 1);
+        __syncthreads();
+        auto p = a.val(first);
+        const int cut = partition_step(a, first, last, p, Lpos, Rasc, lds);
+        if (cut <= first || cut >= last) break;  // impossible for a correct emulation; never loop unbounded
+        if (cut <= nth) first = cut;
+        else last = cut;
+    }
+    if (!heap_done && threadIdx.x == 0) insertion_sort(a, first, last);
+    __syncthreads();
+    // std::partition(begin+npoints, end, response >= ambiguous) (bidirectional)
+    auto amb = a.val(nth);
+    int nL = 0, nR = 0;
+    for (int base = npoints; base < n; base += blockDim.x) {
+        const int i = base + threadIdx.x;
+        const bool in = i < n;
+        int fl = 0, fr = 0;
+        if (in) {
+            bool pr = a.val(i) >= amb;
+            fl = !pr;
+            fr = pr;
+        }
+        int pa, pb, ta, tb;
+        block_excl_scan2(fl, fr, pa, pb, ta, tb, lds);
+        if (fl) Lpos[nL + pa] = i;
+        if (fr) Rasc[nR + pb] = i;
+        nL += ta;
+        nR += tb;
+    }
+    __syncthreads();
+    const int K = min(nL, nR);
+    int cnt = 0;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) cnt += Lpos[k] < Rasc[nR - 1 - k];
+    const int kstar = block_sum(cnt, lds);
+    for (int k = threadIdx.x; k < kstar; k += blockDim.x) a.swap(Lpos[k], Rasc[nR - 1 - k]);
+    __syncthreads();
+    return npoints + nR;
+}
+
+constexpr int kSelNT = 512;
+
+__global__ __launch_bounds__(kSelNT) void select_fast_kernel(StreamParams P) {
+    const int l = blockIdx.x, f = blockIdx.y;
+    if (l >= P.plan.nlevels) return;
+    const LevelGeom& G = P.plan.L[l];
+    __shared__ int lds[64];
+    __shared__ int boff[1024 + 1];
+    const int32_t* bc = P.buf.band_cnt + (int64_t)f * P.plan.total_bands + G.band_base;
+    const uint32_t* bsrc = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off;
+    uint32_t* A = P.buf.cand + (int64_t)f * P.plan.cand_stride + G.cand_off;
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int b = 0; b < G.nbands; ++b) {
+            boff[b] = s;
+            s += bc[b];
+        }
+        boff[G.nbands] = s;
+    }
+    __syncthreads();
+    const int n = boff[G.nbands];
+    for (int b = 0; b < G.nbands; ++b) {
+        const int c = boff[b + 1] - boff[b];
+        for (int i = threadIdx.x; i < c; i += kSelNT) A[boff[b] + i] = bsrc[(int64_t)b * G.band_cap + i];
+    }
+    __syncthreads();
+    int32_t* Lpos = P.buf.sel_tmp + (int64_t)f * 2 * P.plan.cand_stride + 2 * G.cand_off;
+    int32_t* Rasc = Lpos + G.cand_cap;
+    const int k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+    if (threadIdx.x == 0) P.buf.cnt1[f * kMaxLevels + l] = k;
+}
+
+// orb.cpp HarrisResponses(blockSize 7, k 0.04f) on the unblurred level.
+__global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
+    const int l = blockIdx.y, f = blockIdx.z;
+    const int n = P.buf.cnt1[f * kMaxLevels + l];
+    const LevelGeom& G = P.plan.L[l];
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+    const int x0 = key & 0xFFF, y0 = (key >> 12) & 0xFFF;
+    const uint8_t* img = level_ptr(P, f, l);
+    const int step = level_pitch(P, l);
+    const uint8_t* ptr0 = img + (int64_t)(y0 - 3) * step + (x0 - 3);
+    int a = 0, b = 0, c = 0;
+    for (int yy = 0; yy < 7; ++yy) {
+        const uint8_t* r = ptr0 + (int64_t)yy * step;
+#pragma unroll
+        for (int xx = 0; xx < 7; ++xx) {
+            const uint8_t* p = r + xx;
+            int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
+            int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    }
+    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+    const float s4 = scale * scale * scale * scale;
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    const float r = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+    P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i] = r;
+    }
+}
+
+__global__ __launch_bounds__(kSelNT) void select_harris_kernel(StreamParams P) {
+    const int l = blockIdx.x, f = blockIdx.y;
+    if (l >= P.plan.nlevels) return;
+    const LevelGeom& G = P.plan.L[l];
+    __shared__ int lds[64];
+    const int n = P.buf.cnt1[f * kMaxLevels + l];
+    uint32_t* A = P.buf.cand + (int64_t)f * P.plan.cand_stride + G.cand_off;
+    float* R = P.buf.resp + (int64_t)f * P.plan.cand_stride + G.cand_off;
+    int32_t* Lpos = P.buf.sel_tmp + (int64_t)f * 2 * P.plan.cand_stride + 2 * G.cand_off;
+    int32_t* Rasc = Lpos + G.cand_cap;
+    const int k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+    if (threadIdx.x == 0) P.buf.cnt2[f * kMaxLevels + l] = k;
+}
+
+// core fastAtan2 polynomial (degrees), evaluated exactly as the CPU restatement.
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.220446049250313e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.220446049250313e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// One wave per keypoint: ICAngles (integer moments, wave-reduced), then
+// pt *= scale, size = 31*scale, and the 256 rBRIEF bits — lane j evaluates bits
+// j, j+64, j+128, j+192 and a ballot assembles each 64-bit descriptor word.
+__global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
+    const int f = blockIdx.y;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int k = blockIdx.x * 4 + wv;
+    const int32_t* c2 = P.buf.cnt2 + f * kMaxLevels;
+    int total = 0;
+    for (int l = 0; l < P.plan.nlevels; ++l) total += c2[l];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        P.buf.nkp[f] = total;
+        if (total > P.plan.kp_cap) atomicOr(&P.buf.status[f], 1);
+    }
+    if (k >= total || k >= P.plan.kp_cap) return;
+    int l = 0, i = k;
+    while (i >= c2[l]) {
+        i -= c2[l];
+        ++l;
+    }
+    const LevelGeom& G = P.plan.L[l];
+    const uint32_t key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+    const float response = P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+    const int kx = key & 0xFFF, ky = (key >> 12) & 0xFFF;
+    // ---- ICAngles on the unblurred level
+    const uint8_t* img = level_ptr(P, f, l);
+    const int step = level_pitch(P, l);
+    const uint8_t* center = img + (int64_t)ky * step + kx;
+    int m01 = 0, m10 = 0;
+    const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
+    for (int it = 0; it < 16; ++it) {
+        const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
+        if (v <= 15 && (lane & 31) < 31) {
+            const int av = v < 0 ? -v : v;
+            if ((u < 0 ? -u : u) <= c_umax[av]) {
+                const int I = center[(int64_t)v * step + u];
+                m10 += u * I;
+                m01 += v * I;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o);
+        m01 += __shfl_xor(m01, o);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float scale = G.scale;
+    const float ptx = (float)kx * scale, pty = (float)ky * scale;
+    // ---- rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
+    const float sc = 1.f / scale;
+    const float ang = angle * (float)(M_PI / 180.f);
+    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    const uint8_t* bl = blur_ptr(P, f, l);
+    const int bstep = G.w;
+    const uint8_t* bc = bl + (int64_t)cv_round_f(pty * sc) * bstep + cv_round_f(ptx * sc);
+    unsigned long long words[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int bit = q * 64 + lane;
+        const int px0 = c_pattern[bit * 4 + 0], py0 = c_pattern[bit * 4 + 1];
+        const int px1 = c_pattern[bit * 4 + 2], py1 = c_pattern[bit * 4 + 3];
+        float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
+        float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
+        const int t0 = bc[(int64_t)cv_round_f(y0) * bstep + cv_round_f(x0)];
+        const int t1 = bc[(int64_t)cv_round_f(y1) * bstep + cv_round_f(x1)];
+        words[q] = __ballot(t0 < t1);
+    }
+    if (lane == 0) {
+        dvo_keypoint kp;
+        kp.x = ptx;
+        kp.y = pty;
+        kp.size = 31 * scale;
+        kp.angle = angle;
+        kp.response = response;
+        kp.octave = l;
+        kp.class_id = -1;
+        P.buf.kps[(int64_t)f * P.plan.kp_cap + k] = kp;
+        unsigned long long* d = reinterpret_cast<unsigned long long*>(P.buf.desc + ((int64_t)f * P.plan.kp_cap + k) * 32);
+        d[0] = words[0];
+        d[1] = words[1];
+        d[2] = words[2];
+        d[3] = words[3];
+    }
+}
+
+__global__ void test_retain_best_kernel(float* resp, uint32_t* payload, int32_t* tmp, int n, int npoints, int depth,
+                                        int* kout) {
+    __shared__ int lds[64];
+    int k = retain_best_block(HarrisVals{resp, payload}, n, npoints, depth, tmp, tmp + n + 1, lds);
+    if (threadIdx.x == 0) *kout = k;
+}
+
+}  // namespace
+
+hipError_t launch_orb(const StreamParams& P, hipStream_t s) {
+    const Plan& pl = P.plan;
+    const int F = P.nframes;
+    for (int l = 1; l < pl.nlevels; ++l) {
+        dim3 grid((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F);
+        hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
+    }
+    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles, F), dim3(256), 0, s, P);
+    const int SW = ((pl.L[0].w + 3) & ~3) + 16;
+    const size_t fast_lds = (size_t)(16 + 10) * SW;
+    if (pl.total_bands > 0)
+        hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), fast_lds, s, P);
+    hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    // Harris runs over the FAST-retained list, whose length (>= 2n with ties) is
+    // only known on the device: a grid sized for 2n, grid-stride beyond that.
+    int hb = 0;
+    for (int l = 0; l < pl.nlevels; ++l) hb = hb > 2 * pl.L[l].nper ? hb : 2 * pl.L[l].nper;
+    hipLaunchKernelGGL(harris_kernel, dim3((hb + 255) / 256 + 1, pl.nlevels, F), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    hipLaunchKernelGGL(describe_kernel, dim3((pl.kp_cap + 3) / 4, F), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
+                                   int* d_k, hipStream_t s) {
+    hipLaunchKernelGGL(test_retain_best_kernel, dim3(1), dim3(kSelNT), 0, s, d_resp, d_payload, d_tmp, n, n_points,
+                       depth, d_k);
+    return hipGetLastError();
+}
+
+}  // namespace dvo

@@ -1,0 +1,101 @@
+"""Batched frame stream on the GPU: the whole per-pair path of
+VisualOdometry.visual_odometry_calculations (visual_odometry_v3.py:384-408) for
+many device-resident frames per call.
+
+A call with n frames runs ORB on every frame once, matches each consecutive
+pair, runs findEssentialMat(RANSAC) + recoverPose per pair and writes n-1
+256-byte pair records (PAIR_RECORD_DTYPE) to device memory.  Torch tensors are
+only containers for device memory; all compute is in libdvo_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ._native import (DMATCH_DTYPE, KEYPOINT_DTYPE, PAIR_RECORD_DTYPE, Context, StreamConfig, _vp, orb_params, ptr)
+
+
+class FrameStream:
+    def __init__(self, width: int, height: int, K, nfeatures: int = 500, max_frames: int = 64, prob: float = 0.999,
+                 threshold: float = 1.0, max_iters: int = 1000, cross_check: int = 1, dist_thresh: float = 50.0,
+                 device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.device = torch.device("cuda", device)
+        cfg = StreamConfig()
+        cfg.width, cfg.height, cfg.max_frames = int(width), int(height), int(max_frames)
+        cfg.orb = orb_params(nfeatures=nfeatures)
+        K = np.asarray(K, np.float64).reshape(9)
+        for i in range(9):
+            cfg.K[i] = float(K[i])
+        cfg.prob, cfg.threshold, cfg.max_iters = float(prob), float(threshold), int(max_iters)
+        cfg.cross_check, cfg.dist_thresh = int(cross_check), float(dist_thresh)
+        h = _vp()
+        self.ctx.check(self.ctx.lib.dvo_stream_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.width, self.height, self.max_frames, self.nfeatures = width, height, max_frames, nfeatures
+        self.K = K.reshape(3, 3)
+
+    @property
+    def hip_stream(self) -> int:
+        return self.ctx.lib.dvo_stream_hip_stream(self.h) or 0
+
+    def new_records(self, n_pairs: int) -> torch.Tensor:
+        return torch.zeros(max(n_pairs, 1) * PAIR_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+
+    def process(self, frames: torch.Tensor, records: torch.Tensor | None = None) -> torch.Tensor:
+        """Enqueue the batch on the stream's HIP stream (asynchronous)."""
+        if frames.dtype != torch.uint8 or frames.dim() != 3 or not frames.is_cuda:
+            raise ValueError("frames must be a uint8 [n, H, W] device tensor")
+        n, h, w = frames.shape
+        if (h, w) != (self.height, self.width):
+            raise ValueError(f"frame size {w}x{h} != stream {self.width}x{self.height}")
+        if frames.stride(2) != 1 or frames.stride(1) < w:
+            raise ValueError("frames rows must be contiguous")
+        if records is None:
+            records = self.new_records(n - 1)
+        self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
+                                                       frames.stride(1), records.data_ptr() if n > 1 else None))
+        return records
+
+    def sync(self):
+        self.ctx.check(self.ctx.lib.dvo_stream_sync(self.h))
+
+    @staticmethod
+    def records_numpy(records: torch.Tensor, n_pairs: int) -> np.ndarray:
+        raw = records[: n_pairs * PAIR_RECORD_DTYPE.itemsize].cpu().numpy()
+        return raw.view(PAIR_RECORD_DTYPE).copy()
+
+    def features(self, frame: int):
+        cap = self.nfeatures + 1024
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        self.ctx.check(self.ctx.lib.dvo_stream_get_features(self.h, frame, ptr(kps), ptr(desc), cap, ctypes.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def matches(self, pair: int) -> np.ndarray:
+        cap = self.nfeatures + 1024
+        out = np.zeros(cap, DMATCH_DTYPE)
+        m = ctypes.c_int()
+        self.ctx.check(self.ctx.lib.dvo_stream_get_matches(self.h, pair, ptr(out), cap, ctypes.byref(m)))
+        return out[:m.value].copy()
+
+    def pyramid(self, frame: int, level: int, blurred: bool = False) -> np.ndarray:
+        from .plan import level_sizes
+        lw, lh = level_sizes(self.width, self.height)[level]
+        out = np.zeros(lw * lh, np.uint8)
+        self.ctx.check(self.ctx.lib.dvo_stream_get_pyramid(self.h, frame, level, int(blurred), ptr(out), out.size))
+        return out.reshape(lh, lw)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.dvo_stream_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,152 @@
+/* droplet_visual_odometry_amd — C ABI of the MI355X visual-odometry front end.
+ *
+ * This is the drop-in boundary underneath the reference's Python call surface
+ * (scripts/visual_odometry_v3.py, scripts/pose_estimation_module.py).  Each
+ * per-call entry point replaces exactly one OpenCV operator the reference
+ * invokes on its hot path; the batched stream API runs the whole per-pair path
+ * (v3:384-408) for many frames per launch.  All compute runs in hand-written
+ * HIP kernels for gfx950; there is no CPU fallback.
+ *
+ * Conventions: plain pointers and sizes, caller-owned outputs, int status
+ * (DVO_OK or a negative DVO_E* code, message via dvo_last_error).  No C++
+ * exceptions cross this boundary.  One context per host thread.
+ */
+#ifndef DVO_H_
+#define DVO_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVO_OK 0
+#define DVO_EINVAL (-1)   /* bad argument (cv2.error analogue)                     */
+#define DVO_ENOFEAT (-2)  /* no descriptors where the reference would hit None     */
+#define DVO_EFEWPTS (-3)  /* fewer than 5 correspondences: findEssentialMat empty  */
+#define DVO_EHIP (-4)     /* HIP runtime failure                                   */
+#define DVO_ECAP (-5)     /* caller buffer too small; *_out holds the needed size  */
+#define DVO_ENOMODEL (-6) /* RANSAC found no model (E empty)                       */
+
+typedef struct dvo_ctx dvo_ctx;
+typedef struct dvo_stream dvo_stream;
+
+/* cv::KeyPoint as the reference's Python sees it (28 bytes). */
+typedef struct {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} dvo_keypoint;
+
+/* cv::DMatch (16 bytes). */
+typedef struct {
+    int32_t queryIdx, trainIdx, imgIdx;
+    float distance;
+} dvo_dmatch;
+
+/* cv.ORB_create() parameters (visual_odometry_v3.py:96 uses the defaults).
+ * Only the defaults other than nfeatures are implemented; others -> DVO_EINVAL. */
+typedef struct {
+    int32_t nfeatures;      /* 500   */
+    float scale_factor;     /* 1.2f  */
+    int32_t nlevels;        /* 8     */
+    int32_t edge_threshold; /* 31    */
+    int32_t first_level;    /* 0     */
+    int32_t wta_k;          /* 2     */
+    int32_t score_type;     /* 0 = HARRIS_SCORE */
+    int32_t patch_size;     /* 31    */
+    int32_t fast_threshold; /* 20    */
+} dvo_orb_params;
+
+int dvo_version(void);
+int dvo_ctx_create(dvo_ctx** out, int device);
+void dvo_ctx_destroy(dvo_ctx* ctx);
+const char* dvo_last_error(const dvo_ctx* ctx);
+
+/* Replaces cv::ORB::detectAndCompute(img, None) — visual_odometry_v3.py:373.
+ * img: host mono8, `stride` bytes per row.  Writes up to `cap` keypoints and
+ * cap*32 descriptor bytes; *n_out = number found (DVO_ECAP if > cap). */
+int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const uint8_t* img, int w, int h,
+                               int stride, dvo_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+
+/* Replaces cv::BFMatcher(NORM_HAMMING, crossCheck).match(query, train) —
+ * visual_odometry_v3.py:75 (construction) and :219 (call).  Output in
+ * queryIdx order, as OpenCV returns it.  cross_check: 0 off, 1 OpenCV 4.x
+ * mutual nearest neighbour, 2 OpenCV 3.x reverse-pass semantics. */
+int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int cross_check,
+                         dvo_dmatch* out, int cap, int* m_out);
+
+/* Replaces cv::findEssentialMat(points1, points2, K, RANSAC, prob, threshold,
+ * maxIters) — visual_odometry_v3.py:297-300.  p1/p2: m x 2 doubles (pixel
+ * coords, the float32 KeyPoint_convert output widened).  E receives 3 rows
+ * (or 3*k rows when m == 5, as OpenCV); cap 90 doubles.  mask: m bytes 0/1. */
+int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int m, const double* K, double prob,
+                           double threshold, int max_iters, double* E, int* e_rows, uint8_t* mask);
+
+/* Replaces cv::recoverPose(E, points1, points2, K, distanceThresh=50, mask) —
+ * visual_odometry_v3.py:303-306.  R row-major 3x3, t unit 3-vector,
+ * mask_out m bytes 0/255, *good = cheirality count (the Python retval). */
+int dvo_recover_pose(dvo_ctx* ctx, const double* E, int e_rows, const double* p1, const double* p2, int m,
+                     const double* K, double dist_thresh, const uint8_t* mask_in, double* R, double* t,
+                     uint8_t* mask_out, int* good);
+
+/* Replaces cv::triangulatePoints(P1, P2, x1, x2) — visual_odometry_v3.py:265.
+ * P1/P2 row-major 3x4; x1/x2 2 x k row-major; X 4 x k row-major. */
+int dvo_triangulate_points(dvo_ctx* ctx, const double* P1, const double* P2, const double* x1, const double* x2,
+                           int k, double* X);
+
+/* ---------------------------------------------------------------------------
+ * Batched frame stream: the whole per-pair path of visual_odometry_calculations
+ * (v3:384-408: detect both frames, match, E/RANSAC, recoverPose) for n_frames
+ * device-resident frames -> n_frames-1 pair records, one launch sequence on the
+ * stream's HIP stream.  Each frame is detected once and its features serve both
+ * pairs it belongs to (identical outputs to re-detecting, v3:387-392). */
+typedef struct {
+    int32_t width, height, max_frames;
+    dvo_orb_params orb;
+    double K[9];
+    double prob;        /* 0.999 */
+    double threshold;   /* 1.0   */
+    int32_t max_iters;  /* 1000  */
+    int32_t cross_check;/* 1     */
+    double dist_thresh; /* 50.0  */
+} dvo_stream_config;
+
+/* One pair's result, 256 bytes, gathered across ranks by RCCL all-gather. */
+typedef struct {
+    double R[9];
+    double t[3];
+    double E[9];
+    int32_t n_kp_prev, n_kp_cur, n_matches, n_inliers;
+    int32_t n_good, ransac_iters, status, n_models;
+    double reserved[7];
+} dvo_pair_record;
+
+int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** out);
+void dvo_stream_destroy(dvo_stream* s);
+/* d_frames: device pointer, frame i at d_frames + i*frame_stride, rows `stride`
+ * bytes apart.  d_records: device pointer to n_frames-1 records.  Asynchronous
+ * on the stream's HIP stream; call dvo_stream_sync before reading results. */
+int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                       dvo_pair_record* d_records);
+int dvo_stream_sync(dvo_stream* s);
+/* HIP stream the batch runs on (hipStream_t as void*), for event timing. */
+void* dvo_stream_hip_stream(dvo_stream* s);
+/* Host copies of intermediate results of the last dvo_stream_process (tests). */
+int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t* desc, int cap, int* n);
+int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m);
+int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uint8_t* out, int cap);
+
+/* Test hooks: exercise one device algorithm in isolation. */
+/* KeyPointsFilter::retainBest permutation on `n` float responses (GPU emulation
+ * of libstdc++ nth_element + partition); depth < 0 = libstdc++ default. */
+int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int32_t* perm, int* k_out);
+/* RANSACUpdateNumIters on the device for a batch of (ep) values. */
+int dvo_test_update_num_iters(dvo_ctx* ctx, double p, const double* ep, int n, int model_points, int max_iters,
+                              int32_t* out);
+/* 5-point kernel on one sample of 5 normalised correspondences. */
+int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double* models, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DVO_H_ */
