@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/sec of the visual-odometry front end (detect + match + pose).
+
+Workload (BASELINE.json metric / configs[2]): a synthetic 1280x720 mono8
+stream, 2000 ORB features, one MI355X per rank.  One "step" is one batch of B
+new frames: the GPU runs ORB on B+1 device-resident frames (the first is the
+previous batch's last frame), Hamming cross-check matching, findEssentialMat
+(RANSAC, 5-point) and recoverPose for the B consecutive pairs, and with N > 1
+ranks all-gathers the B pair records over RCCL (the pose stream reassembly of
+SURVEY.md §8e).  value = (B x steps x ranks) / max-over-ranks wall time.
+
+Also reported:
+  roofline      the dominant kernel group's algorithmic bytes / its HIP-event
+                time on the library's stream, against 8 TB/s HBM
+  cpu_baseline  the oracle (C++ restatement of the OpenCV path) on one host
+                core over a bounded sample of the same stream (rank 0, N=1)
+
+Run: python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--nfeatures", type=int, default=2000)
+    ap.add_argument("--batch", type=int, default=128, help="new frames per step (pairs per step)")
+    ap.add_argument("--max-iters", type=int, default=1000)
+    ap.add_argument("--pool", type=int, default=0, help="distinct frames rendered per rank (default 2*batch+1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP-event timing")
+    return ap.parse_args()
+
+
+def stage_bytes(w, h, nfeatures, n_matches):
+    """Algorithmic HBM bytes per frame for each kernel group."""
+    from droplet_visual_odometry_amd.plan import level_sizes
+    L = level_sizes(w, h)
+    px = [a * b for a, b in L]
+    n = nfeatures
+    return {
+        "pyramid": float(sum(px[l - 1] + px[l] for l in range(1, 8))),  # read l-1, write l
+        "blur": float(2 * sum(px)),                                    # read + write every level
+        "fast": float(sum(px)),                                        # read every level once
+        "select_harris": float(8 * 2 * n + 81 * 2 * n),                 # keys + 9x9 Harris windows
+        "describe": float(n * (749 + 512 + 28 + 32)),                  # angle disc + pattern + kp + desc
+        "match": float(2 * 2 * n * 32 + 16 * n_matches),               # both directions read both sets
+        "ransac": float(32 * n_matches),                               # normalised correspondences
+        "recover_pose": float(32 * n_matches + 256),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from droplet_visual_odometry_amd._native import Context, PAIR_RECORD_DTYPE
+    from droplet_visual_odometry_amd.plan import algorithmic_bytes_per_frame
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import SceneStream
+
+    W, H, N, B = args.width, args.height, args.nfeatures, args.batch
+    scene = SceneStream(W, H, device=str(dev))
+    pool_n = args.pool or (2 * B + 1)
+    base = rank * 100_000  # each rank owns a disjoint stretch of the stream (weak scaling)
+    pool = torch.stack([scene.render(base + i) for i in range(pool_n)]).contiguous()
+    torch.cuda.synchronize()
+
+    ctx = Context(local_rank)
+    fs = FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
+    rec = fs.new_records(B)
+    gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=dev) if world > 1 else None
+    n_windows = max(1, (pool_n - 1) // B)
+
+    def step(i):
+        s = (i % n_windows) * B
+        fs.process(pool[s:s + B + 1], rec)
+        if world > 1:
+            fs.sync()  # records complete on the library's stream before RCCL reads them
+            dist.all_gather_into_tensor(gathered, rec)
+
+    for i in range(args.warmup):
+        step(i)
+    fs.sync()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        fs.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    fs.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    recs = FrameStream.records_numpy(rec, B)
+    stage_ms, calls = (fs.stage_times() if not args.no_profile else ({}, 0))
+    frames_total = B * args.steps * world
+    value = frames_total / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    m_avg = float(np.mean(recs["n_matches"])) if len(recs) else N / 2
+    ok = int(np.sum(recs["status"] == 0))
+    roofline = None
+    if stage_ms and calls:
+        sb = stage_bytes(W, H, N, m_avg)
+        per_call = {k: v / calls for k, v in stage_ms.items()}
+        dom = max(per_call, key=per_call.get)
+        frames_per_call = B + 1 if dom in ("pyramid", "blur", "fast", "select_harris", "describe") else B
+        bytes_per_launch = sb[dom] * frames_per_call
+        achieved = bytes_per_launch / (per_call[dom] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "kernel": dom,
+                    "kernel_ms_per_launch": round(per_call[dom], 4),
+                    "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
+                    "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
+                    "path_frac": round(value / world * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9
+                                       / HBM_PEAK_GBS, 8)}
+
+    cpu = None
+    if args.cpu_seconds > 0 and world == 1:
+        cpu = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds)
+
+    out = {
+        "metric": "frames/sec (detect+match+pose) at 1280x720, 2000 feats",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/f32/f64",
+        "data": "synthetic (seeded ray-cast textured room, droplet_visual_odometry_amd/synth.py)",
+        "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, batch {B} new frames/step per GPU",
+                   "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
+                   "parallelism": f"frame-sharded x{world}" + (" + RCCL all_gather" if world > 1 else ""),
+                   "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
+                   "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
+    """The oracle (restated OpenCV path, -O2 C++, one core) on the same stream:
+    sequential pairs with the previous frame's features reused (streaming mode)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    frames = pool.cpu().numpy()
+    t0 = time.perf_counter()
+    kp_prev = oracle.detect_and_compute(frames[0], nfeatures)
+    n = 0
+    i = 0
+    while time.perf_counter() - t0 < seconds and i + 1 < len(frames):
+        r = oracle.pair_pose(frames[i], frames[i + 1], K, nfeatures, max_iters=max_iters, kp_prev=kp_prev)
+        kp_prev = (r["kp_cur"], r["desc_cur"])
+        n += 1
+        i += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} consecutive pairs of the same 1280x720 stream ({dt:.1f} s, first frame's detect "
+                      f"included), oracle/ C++ restatement of the OpenCV path, streaming mode"}
+
+
+if __name__ == "__main__":
+    main()

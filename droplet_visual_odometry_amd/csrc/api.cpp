@@ -34,6 +34,12 @@ struct dvo_stream {
     uint8_t* d_frames = nullptr;  // per-call upload slab (max_frames images)
     int last_nframes = 0;
     hipStream_t hs = nullptr;
+    // profiling: event tables per in-flight call, accumulated on query
+    bool profiling = false;
+    std::vector<std::vector<hipEvent_t>> ev_pending;
+    std::vector<std::vector<hipEvent_t>> ev_free;
+    double stage_ms[DVO_NSTAGES] = {0};
+    int prof_calls = 0;
 };
 
 namespace {
@@ -242,17 +248,53 @@ dvo_orb_params default_orb(int nfeatures) {
     return o;
 }
 
+int acquire_events(dvo_stream* s, hipEvent_t** ev) {
+    dvo_ctx* ctx = s->ctx;
+    std::vector<hipEvent_t> e;
+    if (!s->ev_free.empty()) {
+        e = std::move(s->ev_free.back());
+        s->ev_free.pop_back();
+    } else {
+        e.resize(2 * DVO_NSTAGES);
+        for (auto& x : e) HIP_TRY(hipEventCreate(&x));
+    }
+    s->ev_pending.push_back(std::move(e));
+    *ev = s->ev_pending.back().data();
+    return DVO_OK;
+}
+
+// Drain completed event tables into the per-stage totals (blocks on the last).
+int collect_events(dvo_stream* s) {
+    dvo_ctx* ctx = s->ctx;
+    for (auto& e : s->ev_pending) {
+        HIP_TRY(hipEventSynchronize(e[2 * DVO_NSTAGES - 1]));
+        for (int st = 0; st < DVO_NSTAGES; ++st) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e[2 * st], e[2 * st + 1]) == hipSuccess) s->stage_ms[st] += ms;
+        }
+        s->prof_calls++;
+        s->ev_free.push_back(std::move(e));
+    }
+    s->ev_pending.clear();
+    return DVO_OK;
+}
+
 int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, int pitch, dvo_pair_record* d_rec,
                bool detect_only) {
     dvo_ctx* ctx = s->ctx;
     StreamParams P = params_of(s, d_frames, n, fstride, pitch);
+    hipEvent_t* ev = nullptr;
+    if (s->profiling && !detect_only && n >= 2) {
+        int rc = acquire_events(s, &ev);
+        if (rc) return rc;
+    }
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
-    HIP_TRY(launch_orb(P, s->hs));
+    HIP_TRY(launch_orb(P, s->hs, ev));
     s->last_nframes = n;
     if (detect_only || n < 2) return DVO_OK;
-    HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs));
+    HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, ev));
     GeomArgs g = stream_geom(s);
-    HIP_TRY(launch_geometry(P, g, d_rec, s->hs));
+    HIP_TRY(launch_geometry(P, g, d_rec, s->hs, ev));
     return DVO_OK;
 }
 
@@ -321,7 +363,29 @@ void dvo_stream_destroy(dvo_stream* s) {
     hipSetDevice(s->ctx->device);
     hipStreamSynchronize(s->hs);
     for (void* p : s->allocs) hipFree(p);
+    for (auto* pool : {&s->ev_pending, &s->ev_free})
+        for (auto& e : *pool)
+            for (auto x : e) hipEventDestroy(x);
     delete s;
+}
+
+int dvo_stream_set_profiling(dvo_stream* s, int enable) {
+    if (!s) return DVO_EINVAL;
+    int rc = collect_events(s);
+    if (rc) return rc;
+    s->profiling = enable != 0;
+    for (double& v : s->stage_ms) v = 0;
+    s->prof_calls = 0;
+    return DVO_OK;
+}
+
+int dvo_stream_stage_times(dvo_stream* s, double* ms, int* calls) {
+    if (!s || !ms) return DVO_EINVAL;
+    int rc = collect_events(s);
+    if (rc) return rc;
+    for (int i = 0; i < DVO_NSTAGES; ++i) ms[i] = s->stage_ms[i];
+    if (calls) *calls = s->prof_calls;
+    return DVO_OK;
 }
 
 void* dvo_stream_hip_stream(dvo_stream* s) { return s ? (void*)s->hs : nullptr; }

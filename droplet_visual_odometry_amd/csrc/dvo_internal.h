@@ -130,9 +130,14 @@ struct GeomArgs {
 constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;
 
 // ---- host entry points of the kernels (implemented in the .hip files) -------
-hipError_t launch_orb(const StreamParams& P, hipStream_t s);
-hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s);
-hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s);
+// ev: optional table of 2*DVO_NSTAGES events recorded around each stage.
+inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
+    if (ev) hipEventRecord(ev[2 * stage + end], s);
+}
+hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nullptr);
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev = nullptr);
+hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
+                           hipEvent_t* ev = nullptr);
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
 hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,

@@ -1045,12 +1045,19 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
     return hipGetLastError();
 }
 
-hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s) {
+hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
+                           hipEvent_t* ev) {
     const int pairs = P.nframes - 1;
     if (pairs <= 0) return hipSuccess;
-    hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac | kStagePose, s);
+    mark(ev, 6, 0, s);
+    hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac, s);
+    mark(ev, 6, 1, s);
+    if (e != hipSuccess) return e;
+    mark(ev, 7, 0, s);
+    e = launch_geometry_args(g, pairs, kStagePose, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(records_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, P, g, records);
+    mark(ev, 7, 1, s);
     return hipGetLastError();
 }
 

@@ -243,13 +243,15 @@ __global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* nn
 
 }  // namespace
 
-hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s) {
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev) {
     if (P.nframes < 2) return hipSuccess;
+    mark(ev, 5, 0, s);
     const int cap = P.plan.kp_cap;
     const size_t lds = (size_t)(cap < kTrainChunk ? cap : kTrainChunk) * 32;
     dim3 grid((cap + kNNQ - 1) / kNNQ, 2, P.nframes - 1);
     hipLaunchKernelGGL(nn_stream_kernel, grid, dim3(kNNThreads), lds, s, P);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
+    mark(ev, 5, 1, s);
     return hipGetLastError();
 }
 

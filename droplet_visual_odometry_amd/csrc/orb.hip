@@ -743,18 +743,25 @@ __global__ void test_retain_best_kernel(float* resp, uint32_t* payload, int32_t*
 
 }  // namespace
 
-hipError_t launch_orb(const StreamParams& P, hipStream_t s) {
+hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const Plan& pl = P.plan;
     const int F = P.nframes;
+    mark(ev, 0, 0, s);
     for (int l = 1; l < pl.nlevels; ++l) {
         dim3 grid((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F);
         hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
     }
+    mark(ev, 0, 1, s);
+    mark(ev, 1, 0, s);
     hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles, F), dim3(256), 0, s, P);
+    mark(ev, 1, 1, s);
     const int SW = ((pl.L[0].w + 3) & ~3) + 16;
     const size_t fast_lds = (size_t)(16 + 10) * SW;
+    mark(ev, 2, 0, s);
     if (pl.total_bands > 0)
         hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), fast_lds, s, P);
+    mark(ev, 2, 1, s);
+    mark(ev, 3, 0, s);
     hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     // Harris runs over the FAST-retained list, whose length (>= 2n with ties) is
     // only known on the device: a grid sized for 2n, grid-stride beyond that.
@@ -762,7 +769,10 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s) {
     for (int l = 0; l < pl.nlevels; ++l) hb = hb > 2 * pl.L[l].nper ? hb : 2 * pl.L[l].nper;
     hipLaunchKernelGGL(harris_kernel, dim3((hb + 255) / 256 + 1, pl.nlevels, F), dim3(256), 0, s, P);
     hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    mark(ev, 3, 1, s);
+    mark(ev, 4, 0, s);
     hipLaunchKernelGGL(describe_kernel, dim3((pl.kp_cap + 3) / 4, F), dim3(256), 0, s, P);
+    mark(ev, 4, 1, s);
     return hipGetLastError();
 }
 

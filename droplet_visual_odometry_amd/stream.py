@@ -59,6 +59,17 @@ class FrameStream:
                                                        frames.stride(1), records.data_ptr() if n > 1 else None))
         return records
 
+    def set_profiling(self, enable: bool = True):
+        self.ctx.check(self.ctx.lib.dvo_stream_set_profiling(self.h, int(enable)))
+
+    def stage_times(self):
+        """{stage: accumulated device ms} over calls since set_profiling(True), plus call count."""
+        from ._native import DVO_NSTAGES, STAGE_NAMES
+        ms = np.zeros(DVO_NSTAGES, np.float64)
+        calls = ctypes.c_int()
+        self.ctx.check(self.ctx.lib.dvo_stream_stage_times(self.h, ptr(ms), ctypes.byref(calls)))
+        return dict(zip(STAGE_NAMES, ms.tolist())), calls.value
+
     def sync(self):
         self.ctx.check(self.ctx.lib.dvo_stream_sync(self.h))
 

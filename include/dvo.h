@@ -131,6 +131,14 @@ int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int
 int dvo_stream_sync(dvo_stream* s);
 /* HIP stream the batch runs on (hipStream_t as void*), for event timing. */
 void* dvo_stream_hip_stream(dvo_stream* s);
+/* Per-stage device time via HIP events recorded on the stream's HIP stream
+ * around each kernel group (0 pyramid, 1 blur, 2 fast, 3 select+harris,
+ * 4 describe, 5 match, 6 ransac, 7 recoverPose+records).  Accumulated over
+ * every dvo_stream_process since profiling was enabled. */
+#define DVO_NSTAGES 8
+int dvo_stream_set_profiling(dvo_stream* s, int enable);
+int dvo_stream_stage_times(dvo_stream* s, double* ms /* DVO_NSTAGES */, int* calls);
+
 /* Host copies of intermediate results of the last dvo_stream_process (tests). */
 int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t* desc, int cap, int* n);
 int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m);
