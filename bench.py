@@ -5,9 +5,10 @@ Workload (BASELINE.json metric / configs[2]): a synthetic 1280x720 mono8
 stream, 2000 ORB features, one MI355X per rank.  One "step" is one batch of B
 new frames: the GPU runs ORB on B+1 device-resident frames (the first is the
 previous batch's last frame), Hamming cross-check matching, findEssentialMat
-(RANSAC, 5-point) and recoverPose for the B consecutive pairs, and with N > 1
-ranks all-gathers the B pair records over RCCL (the pose stream reassembly of
-SURVEY.md §8e).  value = (B x steps x ranks) / max-over-ranks wall time.
+(RANSAC, 5-point), recoverPose and the marker-scaled pose tail (triangulated
+marker corners -> scale -> 4x4 relative pose -> chained absolute pose) for the B
+consecutive pairs, and with N > 1 ranks all-gathers the B pair records over
+RCCL (the pose stream reassembly of SURVEY.md §8e).  value = (B x steps x ranks) / max-over-ranks wall time.
 
 Also reported:
   roofline      the dominant kernel group's algorithmic bytes / its HIP-event
@@ -64,6 +65,7 @@ def stage_bytes(w, h, nfeatures, n_matches):
         "match": float(2 * 2 * n * 32 + 16 * n_matches),               # both directions read both sets
         "ransac": float(32 * n_matches),                               # normalised correspondences
         "recover_pose": float(32 * n_matches + 256),
+        "pose_tail": float(96 + 16 + 2 * 64 + 2 * 128),                  # R|t, info, corners, T_rel + T_abs
     }
 
 
@@ -96,12 +98,19 @@ def main():
     ctx = Context(local_rank)
     fs = FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
     rec = fs.new_records(B)
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    corners = torch.tensor(np.stack([scene.marker_corners(base + i) for i in range(pool_n)]), dtype=torch.float64,
+                           device=dev)
+    T_rel = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    T_abs = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
+    fs.reset_pose()
     gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=dev) if world > 1 else None
     n_windows = max(1, (pool_n - 1) // B)
 
     def step(i):
         s = (i % n_windows) * B
         fs.process(pool[s:s + B + 1], rec)
+        fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel, T_abs)
         if world > 1:
             fs.sync()  # records complete on the library's stream before RCCL reads them
             dist.all_gather_into_tensor(gathered, rec)

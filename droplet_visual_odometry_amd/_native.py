@@ -28,8 +28,9 @@ DVO_EFEWPTS = -3
 DVO_EHIP = -4
 DVO_ECAP = -5
 DVO_ENOMODEL = -6
-DVO_NSTAGES = 8
-STAGE_NAMES = ["pyramid", "blur", "fast", "select_harris", "describe", "match", "ransac", "recover_pose"]
+DVO_NSTAGES = 9
+STAGE_NAMES = ["pyramid", "blur", "fast", "select_harris", "describe", "match", "ransac", "recover_pose",
+               "pose_tail"]
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
@@ -88,6 +89,8 @@ _SIGNATURES = {
     "dvo_stream_sync": ([_vp], _c),
     "dvo_stream_hip_stream": ([_vp], _vp),
     "dvo_stream_set_profiling": ([_vp, _c], _c),
+    "dvo_stream_reset_pose": ([_vp, _vp, _vp], _c),
+    "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),
     "dvo_stream_get_features": ([_vp, _c, _vp, _vp, _c, _ip], _c),
     "dvo_stream_get_matches": ([_vp, _c, _vp, _c, _ip], _c),

@@ -32,7 +32,9 @@ struct dvo_stream {
     Buffers buf{};
     std::vector<void*> allocs;
     uint8_t* d_frames = nullptr;  // per-call upload slab (max_frames images)
+    double* d_carry = nullptr;    // pose tail carry: P_prev (12) | T_abs_prev (16)
     int last_nframes = 0;
+    bool last_has_pairs = false;  // the last call ran match + geometry
     hipStream_t hs = nullptr;
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
@@ -230,6 +232,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.Rt, (size_t)F * 12);
     A(b.good, (size_t)F);
     A(s->d_frames, (size_t)F * s->cfg.width * s->cfg.height);
+    A(s->d_carry, (size_t)28);
 #undef A
     return DVO_OK;
 }
@@ -291,10 +294,13 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
     HIP_TRY(launch_orb(P, s->hs, ev));
     s->last_nframes = n;
-    if (detect_only || n < 2) return DVO_OK;
+    s->last_has_pairs = !detect_only && n >= 2;
+    if (!s->last_has_pairs) return DVO_OK;
     HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, ev));
     GeomArgs g = stream_geom(s);
     HIP_TRY(launch_geometry(P, g, d_rec, s->hs, ev));
+    mark(ev, 8, 0, s->hs);  // pose-tail pair defaults to 0 ms; dvo_stream_pose_tail re-records it
+    mark(ev, 8, 1, s->hs);
     return DVO_OK;
 }
 
@@ -367,6 +373,34 @@ void dvo_stream_destroy(dvo_stream* s) {
         for (auto& e : *pool)
             for (auto x : e) hipEventDestroy(x);
     delete s;
+}
+
+int dvo_stream_reset_pose(dvo_stream* s, const double* P0, const double* T0) {
+    if (!s || !P0 || !T0) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    double c[28];
+    std::memcpy(c, P0, 12 * sizeof(double));
+    std::memcpy(c + 12, T0, 16 * sizeof(double));
+    HIP_TRY(hipMemcpyAsync(s->d_carry, c, sizeof(c), hipMemcpyHostToDevice, s->hs));
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    return DVO_OK;
+}
+
+int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
+                         double marker_length, double* d_T_rel, double* d_T_abs) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (k < 2 || !d_corners_prev || !d_corners_cur || !d_T_rel || !d_T_abs)
+        return fail(ctx, DVO_EINVAL, "pose tail needs >= 2 corners per frame and output buffers");
+    if (!s->last_has_pairs) return fail(ctx, DVO_EINVAL, "pose tail needs a preceding dvo_stream_process");
+    const int pairs = s->last_nframes - 1;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipEvent_t* ev = (s->profiling && !s->ev_pending.empty()) ? s->ev_pending.back().data() : nullptr;
+    mark(ev, 8, 0, s->hs);
+    HIP_TRY(launch_pose_tail(s->buf.Rt, s->buf.info, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
+                             s->d_carry, d_T_rel, d_T_abs, s->hs));
+    mark(ev, 8, 1, s->hs);
+    return DVO_OK;
 }
 
 int dvo_stream_set_profiling(dvo_stream* s, int enable) {

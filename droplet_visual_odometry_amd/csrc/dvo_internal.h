@@ -139,6 +139,10 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
                            hipEvent_t* ev = nullptr);
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
+// carry: device [12 P_prev | 16 T_abs_prev]; updated in place.
+hipError_t launch_pose_tail(const double* Rt /*[pairs][12]*/, const int32_t* info /*[pairs][4]*/, int pairs,
+                            const double* K, const double* cprev, const double* ccur, int k, double marker_length,
+                            double* carry, double* T_rel, double* T_abs, hipStream_t s);
 hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);

@@ -1025,6 +1025,133 @@ __global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec)
     rec[p] = r;
 }
 
+// ---- pose tail (visual_odometry_v3.py:309-345, :367) -------------------------
+// Gohlke euler_from_matrix(M, 'rxyz') -> (ax, ay, az); rxyz = (firstaxis 2,
+// parity 1, repetition 0, frame 1): i=2, j=1, k=0.
+__device__ void euler_from_matrix_rxyz(const double* R, double& ax, double& ay, double& az) {
+    const int i = 2, j = 1, k = 0;
+    auto M = [&](int r, int c) { return R[r * 3 + c]; };
+    const double eps4 = 4.0 * DBL_EPSILON;
+    double cy = sqrt(M(i, i) * M(i, i) + M(j, i) * M(j, i));
+    if (cy > eps4) {
+        ax = atan2(M(k, j), M(k, k));
+        ay = atan2(-M(k, i), cy);
+        az = atan2(M(j, i), M(i, i));
+    } else {
+        ax = atan2(-M(j, k), M(j, j));
+        ay = atan2(-M(k, i), cy);
+        az = 0.0;
+    }
+    ax = -ax;  // parity
+    ay = -ay;
+    az = -az;
+    double t = ax;  // frame
+    ax = az;
+    az = t;
+}
+
+// Gohlke euler_matrix(ai, aj, ak, 'sxyz') (i=0, j=1, k=2, no parity/repetition/frame).
+__device__ void euler_matrix_sxyz(double ai, double aj, double ak, double* M /*4x4*/) {
+    double si = sin(ai), sj = sin(aj), sk = sin(ak);
+    double ci = cos(ai), cj = cos(aj), ck = cos(ak);
+    double cc = ci * ck, cs = ci * sk, sc = si * ck, ss = si * sk;
+    for (int r = 0; r < 16; ++r) M[r] = (r % 5 == 0) ? 1.0 : 0.0;
+    M[0 * 4 + 0] = cj * ck;
+    M[0 * 4 + 1] = sj * sc - cs;
+    M[0 * 4 + 2] = sj * cc + ss;
+    M[1 * 4 + 0] = cj * sk;
+    M[1 * 4 + 1] = sj * ss + cc;
+    M[1 * 4 + 2] = sj * cs - sc;
+    M[2 * 4 + 0] = -sj;
+    M[2 * 4 + 1] = cj * si;
+    M[2 * 4 + 2] = cj * ci;
+}
+
+__device__ void proj_of(const double* K, const double* Rt, double* P) {  // K . [R | t]
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 4; ++c) {
+            const double a0 = c < 3 ? Rt[0 * 3 + c] : Rt[9 + 0];
+            const double a1 = c < 3 ? Rt[1 * 3 + c] : Rt[9 + 1];
+            const double a2 = c < 3 ? Rt[2 * 3 + c] : Rt[9 + 2];
+            P[r * 4 + c] = K[r * 3 + 0] * a0 + K[r * 3 + 1] * a1 + K[r * 3 + 2] * a2;
+        }
+}
+
+struct TailArgs {
+    const double* Rt;
+    const int32_t* info;
+    int pairs;
+    double K[9];
+    const double* cprev;
+    const double* ccur;
+    int k;
+    double L;
+    double* carry;
+    double* T_rel;
+    double* T_abs;
+};
+
+__global__ void pose_tail_kernel(TailArgs a) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= a.pairs) return;
+    double* Tr = a.T_rel + (int64_t)p * 16;
+    const int32_t* inf = a.info + (int64_t)p * 4;
+    if (!(inf[3] == DVO_OK && inf[0] == 3)) {  // the reference would have raised here
+        for (int r = 0; r < 16; ++r) Tr[r] = (r % 5 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double* Rt = a.Rt + (int64_t)p * 12;
+    double Pc[12], Pp[12];
+    proj_of(a.K, Rt, Pc);
+    if (p == 0) {
+        for (int r = 0; r < 12; ++r) Pp[r] = a.carry[r];
+    } else {
+        proj_of(a.K, a.Rt + (int64_t)(p - 1) * 12, Pp);
+    }
+    double X0[4], X1[4];
+    const double* cp = a.cprev + (int64_t)p * a.k * 2;
+    const double* cc = a.ccur + (int64_t)p * a.k * 2;
+    triangulate_one(Pp, Pc, cp[0], cp[1], cc[0], cc[1], X0);
+    triangulate_one(Pp, Pc, cp[2], cp[3], cc[2], cc[3], X1);
+    const double dx = X0[0] - X1[0], dy = X0[1] - X1[1], dz = X0[2] - X1[2];
+    const double d = sqrt(dx * dx + dy * dy + dz * dz);
+    const double s = a.L / d;
+    double ax, ay, az;
+    euler_from_matrix_rxyz(Rt, ax, ay, az);
+    double M[16];
+    euler_matrix_sxyz(ax, ay, az, M);
+    const double tx = Rt[9] * s, ty = Rt[10] * s, tz = Rt[11] * s;
+    // translation_matrix(t) . M: rows 0..2 gain t * M[3][:] (M[3] = [0 0 0 1])
+    for (int c = 0; c < 4; ++c) {
+        Tr[0 * 4 + c] = M[0 * 4 + c] + tx * M[3 * 4 + c];
+        Tr[1 * 4 + c] = M[1 * 4 + c] + ty * M[3 * 4 + c];
+        Tr[2 * 4 + c] = M[2 * 4 + c] + tz * M[3 * 4 + c];
+        Tr[3 * 4 + c] = M[3 * 4 + c];
+    }
+}
+
+// Sequential prefix product T_abs[p] = T_abs[p-1] . T_rel[p] (one thread; B 4x4
+// products) and carry-out of P_prev / T_abs for the next batch.
+__global__ void pose_chain_kernel(TailArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double T[16], U[16];
+    for (int r = 0; r < 16; ++r) T[r] = a.carry[12 + r];
+    int last_ok = -1;
+    for (int p = 0; p < a.pairs; ++p) {
+        const double* Tr = a.T_rel + (int64_t)p * 16;
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c)
+                U[r * 4 + c] = T[r * 4 + 0] * Tr[0 * 4 + c] + T[r * 4 + 1] * Tr[1 * 4 + c] + T[r * 4 + 2] * Tr[2 * 4 + c] +
+                               T[r * 4 + 3] * Tr[3 * 4 + c];
+        for (int r = 0; r < 16; ++r) T[r] = U[r];
+        for (int r = 0; r < 16; ++r) a.T_abs[(int64_t)p * 16 + r] = T[r];
+        const int32_t* inf = a.info + (int64_t)p * 4;
+        if (inf[3] == DVO_OK && inf[0] == 3) last_ok = p;
+    }
+    if (last_ok >= 0) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
+    for (int r = 0; r < 16; ++r) a.carry[12 + r] = T[r];
+}
+
 __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, int mp, int mi, int32_t* out) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) out[i] = ransac_update_num_iters(p, ep[i], mp, mi);
@@ -1064,6 +1191,27 @@ hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_re
 hipError_t launch_triangulate(const double* d_P, const double* d_x, int k, double* d_X, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     hipLaunchKernelGGL(triangulate_kernel, dim3((k + 255) / 256), dim3(256), 0, s, d_P, d_x, k, d_X);
+    return hipGetLastError();
+}
+
+hipError_t launch_pose_tail(const double* Rt, const int32_t* info, int pairs, const double* K, const double* cprev,
+                            const double* ccur, int k, double marker_length, double* carry, double* T_rel,
+                            double* T_abs, hipStream_t s) {
+    if (pairs <= 0) return hipSuccess;
+    TailArgs a{};
+    a.Rt = Rt;
+    a.info = info;
+    a.pairs = pairs;
+    for (int i = 0; i < 9; ++i) a.K[i] = K[i];
+    a.cprev = cprev;
+    a.ccur = ccur;
+    a.k = k;
+    a.L = marker_length;
+    a.carry = carry;
+    a.T_rel = T_rel;
+    a.T_abs = T_abs;
+    hipLaunchKernelGGL(pose_tail_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(pose_chain_kernel, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

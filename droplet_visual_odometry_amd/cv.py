@@ -1,0 +1,335 @@
+"""The slice of the `cv2` API the reference's hot path uses, backed by the MI355X kernels.
+
+The reference calls (scripts/visual_odometry_v3.py):
+  cv.ORB_create()                                       :96
+  cv.BFMatcher(normType=NORM_HAMMING, crossCheck=True)  :75    .match :219
+  detector.detectAndCompute(img, None)                  :373
+  cv.drawKeypoints(img, kps, None, color, flags=0)      :375   (result discarded, D6)
+  cv.KeyPoint_convert(kps)                              :355, :358
+  cv.findEssentialMat(points1=, points2=, cameraMatrix=, method=RANSAC, prob=, threshold=)   :297
+  cv.recoverPose(E=, points1=, points2=, cameraMatrix=) :303
+  cv.triangulatePoints(projMatr1=, projMatr2=, projPoints1=, projPoints2=)                 :265
+These keep OpenCV's Python signatures, return types and failure points
+(`cv.error` where cv2 raises cv2.error).  Pre-processing helpers used by
+ros_img_msg_to_opencv_image (imdecode, cvtColor, undistort,
+getOptimalNewCameraMatrix; v3:110-135) are outside the GPU hot path (SURVEY.md
+§8f, "next") and are implemented on the host with the restrictions documented
+on each.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import ops
+from ._native import DVOError
+
+# cv2 constants used by the reference
+NORM_L1 = 2
+NORM_L2 = 4
+NORM_HAMMING = 6
+NORM_HAMMING2 = 7
+RANSAC = 8
+LMEDS = 4
+IMREAD_COLOR = 1
+IMREAD_GRAYSCALE = 0
+COLOR_BGR2GRAY = 6
+COLOR_GRAY2BGR = 8
+DrawMatchesFlags_DEFAULT = 0
+DrawMatchesFlags_NOT_DRAW_SINGLE_POINTS = 2
+
+
+class error(Exception):
+    """cv2.error analogue."""
+
+
+class KeyPoint:
+    """cv2.KeyPoint (pt, size, angle, response, octave, class_id)."""
+    __slots__ = ("pt", "size", "angle", "response", "octave", "class_id")
+
+    def __init__(self, x=0.0, y=0.0, size=0.0, angle=-1.0, response=0.0, octave=0, class_id=-1):
+        self.pt = (float(x), float(y))
+        self.size = float(size)
+        self.angle = float(angle)
+        self.response = float(response)
+        self.octave = int(octave)
+        self.class_id = int(class_id)
+
+    def __repr__(self):
+        return f"<KeyPoint pt={self.pt} size={self.size} angle={self.angle} response={self.response} octave={self.octave}>"
+
+
+class DMatch:
+    """cv2.DMatch.  `m[0]` returns `m` itself so the reference's ORB loop
+    (v3:233-238, written for k-NN match lists) runs unchanged."""
+    __slots__ = ("queryIdx", "trainIdx", "imgIdx", "distance")
+
+    def __init__(self, queryIdx=-1, trainIdx=-1, imgIdx=0, distance=float("inf")):
+        self.queryIdx = int(queryIdx)
+        self.trainIdx = int(trainIdx)
+        self.imgIdx = int(imgIdx)
+        self.distance = float(distance)
+
+    def __getitem__(self, i):
+        if i == 0 or i == -1:
+            return self
+        raise IndexError("DMatch index out of range")
+
+    def __repr__(self):
+        return f"<DMatch q={self.queryIdx} t={self.trainIdx} d={self.distance}>"
+
+
+class KeyPointTuple(tuple):
+    """The tuple of KeyPoint objects detectAndCompute returns, carrying the raw
+    structured array (KEYPOINT_DTYPE) so KeyPoint_convert needs no Python loop."""
+    array: np.ndarray
+
+
+def _keypoints_from_array(arr: np.ndarray) -> KeyPointTuple:
+    rows = arr.tolist()
+    t = KeyPointTuple(KeyPoint(*r) for r in rows)
+    t.array = arr
+    return t
+
+
+def KeyPoint_convert(keypoints, keypointIndexes=None):
+    """float32[N, 2] of keypoint coordinates (cv2.KeyPoint_convert)."""
+    arr = getattr(keypoints, "array", None)
+    if arr is not None and keypointIndexes is None:
+        return np.stack([arr["x"], arr["y"]], axis=1).astype(np.float32)
+    kps = keypoints if keypointIndexes is None else [keypoints[i] for i in keypointIndexes]
+    if len(kps) == 0:
+        return np.zeros((0, 2), np.float32)
+    return np.array([k.pt for k in kps], dtype=np.float32)
+
+
+class ORB:
+    """cv2.ORB with the ORB_create() defaults (v3:96); nfeatures configurable."""
+
+    def __init__(self, nfeatures=500, scaleFactor=1.2, nlevels=8, edgeThreshold=31, firstLevel=0, WTA_K=2,
+                 scoreType=0, patchSize=31, fastThreshold=20):
+        if (np.float32(scaleFactor) != np.float32(1.2) or nlevels != 8 or edgeThreshold != 31 or firstLevel != 0
+                or WTA_K != 2 or scoreType != 0 or patchSize != 31):
+            raise error("only the cv.ORB_create() defaults (other than nfeatures/fastThreshold) are implemented")
+        self.nfeatures = int(nfeatures)
+        self.fastThreshold = int(fastThreshold)
+
+    def getMaxFeatures(self):
+        return self.nfeatures
+
+    def setMaxFeatures(self, n):
+        self.nfeatures = int(n)
+
+    def detectAndCompute(self, image, mask, descriptors=None, useProvidedKeypoints=False):
+        if mask is not None:
+            raise error("ORB masks are not supported (the reference passes None, v3:373)")
+        if useProvidedKeypoints:
+            raise error("useProvidedKeypoints is not supported")
+        img = _gray(image)
+        try:
+            kps, desc = ops.detect_and_compute(img, self.nfeatures, self.fastThreshold)
+        except DVOError as e:
+            raise error(str(e)) from e
+        return _keypoints_from_array(kps), (desc if len(kps) else None)
+
+    def detect(self, image, mask=None):
+        return self.detectAndCompute(image, mask)[0]
+
+
+def ORB_create(nfeatures=500, scaleFactor=1.2, nlevels=8, edgeThreshold=31, firstLevel=0, WTA_K=2, scoreType=0,
+               patchSize=31, fastThreshold=20):
+    return ORB(nfeatures, scaleFactor, nlevels, edgeThreshold, firstLevel, WTA_K, scoreType, patchSize, fastThreshold)
+
+
+class BFMatcher:
+    """cv2.BFMatcher; NORM_HAMMING only (the ORB branch, v3:75, v3:97).
+
+    crossCheck follows OpenCV 4.x (mutual nearest neighbour) unless
+    legacy_crosscheck=True selects OpenCV 3.x's reverse-pass semantics."""
+
+    def __init__(self, normType=NORM_L2, crossCheck=False, legacy_crosscheck=False):
+        self.normType = normType
+        self.crossCheck = bool(crossCheck)
+        self.legacy_crosscheck = bool(legacy_crosscheck)
+
+    def match(self, queryDescriptors, trainDescriptors, mask=None):
+        if mask is not None:
+            raise error("match masks are not supported")
+        if queryDescriptors is None or trainDescriptors is None:
+            raise error("(-215:Assertion failed) descriptors must not be empty")
+        if self.normType not in (NORM_HAMMING,):
+            raise error("only NORM_HAMMING (ORB) is implemented on the GPU; SIFT/SURF/FLANN modes are §8f 'next'")
+        q = np.asarray(queryDescriptors)
+        t = np.asarray(trainDescriptors)
+        if q.dtype != np.uint8 or t.dtype != np.uint8 or q.shape[-1] != 32 or t.shape[-1] != 32:
+            raise error("(-215:Assertion failed) NORM_HAMMING needs uint8 descriptors of 32 bytes")
+        mode = 0 if not self.crossCheck else (2 if self.legacy_crosscheck else 1)
+        try:
+            m = ops.bf_match(q, t, mode)
+        except DVOError as e:
+            raise error(str(e)) from e
+        return [DMatch(int(a), int(b), 0, float(d)) for a, b, d in zip(m["queryIdx"], m["trainIdx"], m["distance"])]
+
+    def knnMatch(self, *a, **k):
+        raise error("knnMatch (SIFT/SURF/knn_sift modes) is outside the ORB hot path (SURVEY.md §8f rank 4)")
+
+
+def findEssentialMat(points1, points2, cameraMatrix=None, method=RANSAC, prob=0.999, threshold=1.0, maxIters=1000,
+                     mask=None, **kw):
+    """(E, mask) like cv2.findEssentialMat(..., RANSAC); (None, None) where OpenCV returns an empty E."""
+    if cameraMatrix is None:
+        raise error("cameraMatrix is required")
+    if method != RANSAC:
+        raise error("only method=cv.RANSAC is implemented (v3:299)")
+    p1 = np.asarray(points1, np.float64).reshape(-1, 2)
+    p2 = np.asarray(points2, np.float64).reshape(-1, 2)
+    if len(p1) != len(p2):
+        raise error("(-215:Assertion failed) npoints >= 0 && points2.checkVector(2) == npoints")
+    try:
+        return ops.find_essential_mat(p1, p2, cameraMatrix, prob, threshold, maxIters)
+    except DVOError as e:
+        if e.code in (-3, -6):  # fewer than 5 points / no model: OpenCV returns an empty E
+            return None, None
+        raise error(str(e)) from e
+
+
+def recoverPose(E, points1, points2, cameraMatrix=None, R=None, t=None, mask=None, distanceThresh=50.0, **kw):
+    """(retval, R, t, mask) like cv2.recoverPose(E, points1, points2, cameraMatrix)."""
+    if E is None or np.asarray(E).size == 0:
+        raise error("(-215:Assertion failed) E.cols == 3 && E.rows == 3 in function 'decomposeEssentialMat'")
+    E = np.asarray(E, np.float64)
+    if E.shape != (3, 3):
+        raise error("(-215:Assertion failed) E.cols == 3 && E.rows == 3 in function 'decomposeEssentialMat'")
+    if cameraMatrix is None:
+        raise error("cameraMatrix is required")
+    p1 = np.asarray(points1, np.float64).reshape(-1, 2)
+    p2 = np.asarray(points2, np.float64).reshape(-1, 2)
+    try:
+        return ops.recover_pose(E, p1, p2, cameraMatrix, distanceThresh, mask)
+    except DVOError as e:
+        raise error(str(e)) from e
+
+
+def triangulatePoints(projMatr1, projMatr2, projPoints1, projPoints2, points4D=None):
+    if projMatr1 is None or projMatr2 is None:
+        raise error("(-215:Assertion failed) projection matrices must be 3x4")
+    P1 = np.asarray(projMatr1, np.float64)
+    P2 = np.asarray(projMatr2, np.float64)
+    if P1.shape != (3, 4) or P2.shape != (3, 4):
+        raise error("(-215:Assertion failed) projection matrices must be 3x4")
+    try:
+        return ops.triangulate_points(P1, P2, projPoints1, projPoints2)
+    except DVOError as e:
+        raise error(str(e)) from e
+
+
+# ---- host-side helpers outside the GPU hot path ------------------------------
+def _gray(image):
+    img = np.asarray(image)
+    if img.ndim == 3 and img.shape[2] == 3:
+        return cvtColor(img, COLOR_BGR2GRAY)
+    if img.ndim != 2 or img.dtype != np.uint8:
+        raise error("expected a mono8 or BGR8 image")
+    return img
+
+
+def cvtColor(src, code):
+    """COLOR_BGR2GRAY with OpenCV's 8-bit fixed point (R 4899, G 9617, B 1868, >> 14)."""
+    src = np.asarray(src)
+    if code == COLOR_BGR2GRAY:
+        if src.ndim == 2:
+            return src.copy()
+        b = src[..., 0].astype(np.int32)
+        g = src[..., 1].astype(np.int32)
+        r = src[..., 2].astype(np.int32)
+        return ((b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14).astype(np.uint8)
+    if code == COLOR_GRAY2BGR:
+        return np.repeat(src[..., None], 3, axis=2)
+    raise error(f"cvtColor code {code} not supported")
+
+
+def imdecode(buf, flags=IMREAD_COLOR):
+    """JPEG/PNG decode (PIL) to BGR8 (IMREAD_COLOR) or mono8; None on failure, like cv2."""
+    import io
+    try:
+        from PIL import Image
+        im = Image.open(io.BytesIO(np.asarray(buf, np.uint8).tobytes()))
+        if flags == IMREAD_GRAYSCALE:
+            return np.asarray(im.convert("L"))
+        return np.ascontiguousarray(np.asarray(im.convert("RGB"))[..., ::-1])
+    except Exception:
+        return None
+
+
+def getOptimalNewCameraMatrix(cameraMatrix, distCoeffs, imageSize, alpha, newImgSize=None, centerPrincipalPoint=False):
+    """Zero-distortion case only: the undistorted image equals the input and the
+    camera matrix is unchanged.  Lens undistortion (remap) is SURVEY.md §8f rank 1."""
+    d = np.asarray(distCoeffs, np.float64)
+    if np.any(d != 0):
+        raise error("getOptimalNewCameraMatrix/undistort with non-zero distortion is not implemented yet "
+                    "(SURVEY.md §8f 'next'); feed undistorted mono8 frames")
+    w, h = imageSize
+    return np.asarray(cameraMatrix, np.float64).copy(), (0, 0, int(w), int(h))
+
+
+def undistort(src, cameraMatrix, distCoeffs, dst=None, newCameraMatrix=None):
+    d = np.asarray(distCoeffs, np.float64)
+    if np.any(d != 0):
+        raise error("undistort with non-zero distortion is not implemented yet (SURVEY.md §8f 'next')")
+    if newCameraMatrix is not None and not np.array_equal(np.asarray(newCameraMatrix, np.float64),
+                                                          np.asarray(cameraMatrix, np.float64)):
+        raise error("undistort with newCameraMatrix != cameraMatrix is not implemented yet (SURVEY.md §8f)")
+    return np.array(src, copy=True)
+
+
+_CIRCLE3 = [(dx, dy) for dx in range(-3, 4) for dy in range(-3, 4) if round((dx * dx + dy * dy) ** 0.5) == 3]
+
+
+def drawKeypoints(image, keypoints, outImage=None, color=(0, 255, 0), flags=0):
+    """BGR copy of `image` with a radius-3 circle at every keypoint (DEFAULT flag).
+    The reference computes and discards this image (v3:375, D6)."""
+    img = np.asarray(image)
+    out = np.repeat(img[..., None], 3, axis=2).copy() if img.ndim == 2 else img.copy()
+    arr = getattr(keypoints, "array", None)
+    if arr is not None:
+        xs = np.rint(arr["x"]).astype(np.int64)
+        ys = np.rint(arr["y"]).astype(np.int64)
+    else:
+        xs = np.array([int(round(k.pt[0])) for k in keypoints], np.int64)
+        ys = np.array([int(round(k.pt[1])) for k in keypoints], np.int64)
+    h, w = out.shape[:2]
+    col = np.asarray(color[:3], np.uint8)
+    for dx, dy in _CIRCLE3:
+        x, y = xs + dx, ys + dy
+        ok = (x >= 0) & (x < w) & (y >= 0) & (y < h)
+        out[y[ok], x[ok]] = col
+    return out
+
+
+class _XFeatures2d:
+    @staticmethod
+    def SIFT_create(*a, **k):
+        raise error("SIFT is outside the ORB hot path (SURVEY.md §8f rank 4)")
+
+    @staticmethod
+    def SURF_create(*a, **k):
+        raise error("SURF is outside the ORB hot path (SURVEY.md §8f rank 4)")
+
+
+xfeatures2d = _XFeatures2d()
+
+
+def imshow(*a, **k):  # visualisation helpers are out of scope
+    raise error("imshow is not available (no GUI)")
+
+
+def waitKey(*a, **k):
+    return -1
+
+
+def imwrite(path, img):
+    from PIL import Image
+    arr = np.asarray(img)
+    if arr.ndim == 3:
+        arr = arr[..., ::-1]
+    Image.fromarray(arr).save(path)
+    return True

@@ -59,6 +59,27 @@ class FrameStream:
                                                        frames.stride(1), records.data_ptr() if n > 1 else None))
         return records
 
+    def reset_pose(self, P0=None, T0=None):
+        """Carry-in of the pose tail: P_prev (3x4, default K[I|0] as in controlled
+        mode, v3:164-166) and the absolute pose (4x4, default identity)."""
+        P0 = self.K @ np.hstack((np.eye(3), np.zeros((3, 1)))) if P0 is None else np.asarray(P0, np.float64)
+        T0 = np.eye(4) if T0 is None else np.asarray(T0, np.float64)
+        self.ctx.check(self.ctx.lib.dvo_stream_reset_pose(self.h, ptr(np.ascontiguousarray(P0)),
+                                                          ptr(np.ascontiguousarray(T0))))
+
+    def pose_tail(self, corners_prev: torch.Tensor, corners_cur: torch.Tensor, marker_length: float,
+                  T_rel: torch.Tensor | None = None, T_abs: torch.Tensor | None = None):
+        """Device pose tail for the last processed batch (see dvo.h); corners are
+        float64 [pairs, k, 2] device tensors.  Returns (T_rel, T_abs) [pairs, 4, 4]."""
+        pairs, k = corners_prev.shape[0], corners_prev.shape[1]
+        if T_rel is None:
+            T_rel = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
+        if T_abs is None:
+            T_abs = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
+        self.ctx.check(self.ctx.lib.dvo_stream_pose_tail(self.h, corners_prev.data_ptr(), corners_cur.data_ptr(), k,
+                                                         float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
+        return T_rel, T_abs
+
     def set_profiling(self, enable: bool = True):
         self.ctx.check(self.ctx.lib.dvo_stream_set_profiling(self.h, int(enable)))
 

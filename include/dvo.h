@@ -131,11 +131,25 @@ int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int
 int dvo_stream_sync(dvo_stream* s);
 /* HIP stream the batch runs on (hipStream_t as void*), for event timing. */
 void* dvo_stream_hip_stream(dvo_stream* s);
+/* Pose tail of get_transformation_between_two_frames (v3:309-345) and
+ * previous_current_matching (v3:367) for the pairs of the last
+ * dvo_stream_process, on the device:
+ *   P_cur = K [R | t];  X = triangulatePoints(P_prev, P_cur, c_prev, c_cur);
+ *   d = |X[:3,0] - X[:3,1]| (homogeneous, not divided by W: D3);  s = L / d;
+ *   T_rel = translation_matrix(t s) . euler_matrix(euler_from_matrix(R,'rxyz'),'sxyz');
+ *   T_abs = T_abs_prev . T_rel.
+ * P_prev / T_abs_prev carry over between calls on the device; set them with
+ * dvo_stream_reset_pose (controlled mode: P0 = K [I | 0], v3:164-166).
+ * d_corners_*: device [pairs][k][2] doubles (k >= 2).  Outputs device [pairs][16]. */
+int dvo_stream_reset_pose(dvo_stream* s, const double* P0 /* host 12 */, const double* T0 /* host 16 */);
+int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
+                         double marker_length, double* d_T_rel, double* d_T_abs);
+
 /* Per-stage device time via HIP events recorded on the stream's HIP stream
  * around each kernel group (0 pyramid, 1 blur, 2 fast, 3 select+harris,
- * 4 describe, 5 match, 6 ransac, 7 recoverPose+records).  Accumulated over
+ * 4 describe, 5 match, 6 ransac, 7 recoverPose+records, 8 pose tail).  Accumulated over
  * every dvo_stream_process since profiling was enabled. */
-#define DVO_NSTAGES 8
+#define DVO_NSTAGES 9  /* ... 8 pose tail */
 int dvo_stream_set_profiling(dvo_stream* s, int enable);
 int dvo_stream_stage_times(dvo_stream* s, double* ms /* DVO_NSTAGES */, int* calls);
 

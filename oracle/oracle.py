@@ -239,3 +239,48 @@ def pair_pose(img_prev, img_cur, K, nfeatures=500, max_iters=1000, kp_prev=None)
     good, R, tv, _ = recover_pose(E, p1, p2, K)
     out.update(R=R, t_unit=tv, good=good)
     return out
+
+
+def _euler_from_matrix_rxyz(R):
+    """Gohlke euler_from_matrix(R, 'rxyz') (the `transformations` package call at
+    visual_odometry_v3.py:334): i=2, j=1, k=0, parity, rotating frame."""
+    import math
+    i, j, k = 2, 1, 0
+    cy = math.sqrt(R[i, i] * R[i, i] + R[j, i] * R[j, i])
+    if cy > np.finfo(float).eps * 4.0:
+        ax, ay, az = math.atan2(R[k, j], R[k, k]), math.atan2(-R[k, i], cy), math.atan2(R[j, i], R[i, i])
+    else:
+        ax, ay, az = math.atan2(-R[j, k], R[j, j]), math.atan2(-R[k, i], cy), 0.0
+    ax, ay, az = -ax, -ay, -az
+    return az, ay, ax
+
+
+def _euler_matrix_sxyz(ai, aj, ak):
+    """Gohlke euler_matrix(ai, aj, ak, 'sxyz') (visual_odometry_v3.py:140)."""
+    import math
+    si, sj, sk = math.sin(ai), math.sin(aj), math.sin(ak)
+    ci, cj, ck = math.cos(ai), math.cos(aj), math.cos(ak)
+    cc, cs, sc, ss = ci * ck, ci * sk, si * ck, si * sk
+    M = np.identity(4)
+    M[0, :3] = (cj * ck, sj * sc - cs, sj * cc + ss)
+    M[1, :3] = (cj * sk, sj * ss + cc, sj * cs - sc)
+    M[2, :3] = (-sj, cj * si, cj * ci)
+    return M
+
+
+def pose_tail(K, R, t, corners_prev, corners_cur, marker_length, P_prev, T_prev):
+    """One pair of get_transformation_between_two_frames' tail (visual_odometry_v3.py:
+    309-345) and the chain of previous_current_matching (v3:367):
+    P_cur = K[R|t]; X = triangulatePoints(P_prev, P_cur, c_prev.T, c_cur.T);
+    d = |X[:3,0]-X[:3,1]| (homogeneous, v3:283-289); s = L/d;
+    T_rel = translation_matrix(t s) . euler_matrix(euler_from_matrix(R,'rxyz'),'sxyz').
+    Returns (P_cur, T_rel, T_abs = T_prev . T_rel)."""
+    K = np.asarray(K, np.float64)
+    P_cur = K.dot(np.hstack((R, np.asarray(t, np.float64).reshape(3, 1))))
+    X = triangulate(P_prev, P_cur, np.ascontiguousarray(np.asarray(corners_prev, np.float64).T),
+                    np.ascontiguousarray(np.asarray(corners_cur, np.float64).T))
+    d = float(np.sqrt((X[0, 0] - X[0, 1]) ** 2 + (X[1, 0] - X[1, 1]) ** 2 + (X[2, 0] - X[2, 1]) ** 2))
+    s = marker_length / d
+    T_rel = _euler_matrix_sxyz(*_euler_from_matrix_rxyz(np.asarray(R, np.float64)))
+    T_rel[:3, 3] = np.asarray(t, np.float64).ravel() * s
+    return P_cur, T_rel, np.asarray(T_prev, np.float64).dot(T_rel)

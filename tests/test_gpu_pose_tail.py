@@ -1,0 +1,52 @@
+"""Device pose tail (dvo_stream_pose_tail) vs the host restatement of
+visual_odometry_v3.py:309-345 / :367 (oracle.pose_tail), chained across two
+batches so the device carry (P_prev, T_abs) is exercised.
+
+Tolerance: the tail is float64 arithmetic with libm atan2/sin/cos/sqrt on both
+sides (ocml on the device, glibc on the host, each <= 1 ulp off) and numpy's
+3x3 / 4x4 products; 1e-9 relative on every entry of T_rel and T_abs."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pose_tail_two_batches(gpu_ctx, oracle_mod):
+    import torch
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    frames, K = synth_frames(640, 480, range(7))
+    corners = np.stack([marker_corners(i, K) for i in range(7)])
+    fs = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    fs.reset_pose()
+    P = K @ np.hstack((np.eye(3), np.zeros((3, 1))))
+    T = np.eye(4)
+    dc = torch.from_numpy(corners).cuda()
+    for start in (0, 3):
+        dev = torch.from_numpy(frames[start:start + 4]).cuda()
+        rec = fs.process(dev)
+        T_rel, T_abs = fs.pose_tail(dc[start:start + 3], dc[start + 1:start + 4], MARKER_LEN)
+        fs.sync()
+        recs = FrameStream.records_numpy(rec, 3)
+        T_rel, T_abs = T_rel.cpu().numpy(), T_abs.cpu().numpy()
+        for p in range(3):
+            r = recs[p]
+            assert r["status"] == 0
+            P, Tr, T = oracle_mod.pose_tail(K, r["R"].reshape(3, 3), r["t"], corners[start + p],
+                                            corners[start + p + 1], MARKER_LEN, P, T)
+            np.testing.assert_allclose(T_rel[p], Tr, rtol=1e-9, atol=1e-12)
+            np.testing.assert_allclose(T_abs[p], T, rtol=1e-9, atol=1e-12)
+    fs.close()
+
+
+def test_pose_tail_requires_process(gpu_ctx):
+    import torch
+    from droplet_visual_odometry_amd._native import DVOError
+    from droplet_visual_odometry_amd.stream import FrameStream
+    K = np.array([[500.0, 0, 320], [0, 500, 240], [0, 0, 1]])
+    fs = FrameStream(640, 480, K, nfeatures=500, max_frames=2, ctx=gpu_ctx)
+    c = torch.zeros((1, 4, 2), dtype=torch.float64, device="cuda")
+    with pytest.raises(DVOError):
+        fs.pose_tail(c, c, 0.1)
+    fs.close()
