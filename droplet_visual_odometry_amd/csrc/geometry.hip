@@ -1019,7 +1019,11 @@ __global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec)
     r.n_inliers = info[1];
     r.n_good = ok ? g.good[p] : 0;
     r.ransac_iters = info[2];
-    r.status = (P.buf.status[p] | P.buf.status[p + 1]) ? DVO_ECAP : info[3];
+    // ECAP (a buffer overflowed) > ENOFEAT (an empty frame: the reference's
+    // bf.match(None, ...) raises, v3:219) > the RANSAC / pose status.
+    r.status = (P.buf.status[p] | P.buf.status[p + 1])         ? DVO_ECAP
+               : (P.buf.nkp[p] == 0 || P.buf.nkp[p + 1] == 0) ? DVO_ENOFEAT
+                                                              : info[3];
     r.n_models = info[0] / 3;
     for (int k = 0; k < 7; ++k) r.reserved[k] = 0.0;
     rec[p] = r;

@@ -1,0 +1,56 @@
+"""The drop-in VisualOdometry driven the way trajectory_evaluation_dual_process.py
+drives the reference (dual:151-166: ros_img_msg_to_opencv_image on each
+message, visual_odometry_calculations with the previous absolute pose and the
+marker corners), over a synthetic 640x480 usb_raw stream, against the oracle
+pair path + the host pose-tail restatement.  R, t, E bit-exact; the 4x4 poses
+(numpy / libm on both sides, same operation order) within 1e-12."""
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+
+from conftest import synth_frames
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _yaml(K):
+    d = ", ".join(repr(float(v)) for v in K.ravel())
+    return (f"camera_matrix:\n  rows: 3\n  cols: 3\n  data: [{d}]\n"
+            "distortion_coefficients:\n  rows: 1\n  cols: 5\n  data: [0.0, 0.0, 0.0, 0.0, 0.0]\n")
+
+
+def test_visual_odometry_replay(gpu_ctx, oracle_mod, tmp_path):
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    sys.path.insert(0, os.path.join(ROOT, "droplet_visual_odometry_amd", "dropin"))
+    try:
+        import visual_odometry_v3 as v3
+    finally:
+        sys.path.pop(0)
+    frames, K = synth_frames(640, 480, range(5))
+    y = tmp_path / "cal.yaml"
+    y.write_text(_yaml(K))
+    vo = v3.VisualOdometry(mode="orb", calibration_file_path=str(y), controlled=True, real_marker_length=MARKER_LEN)
+    msgs = [types.SimpleNamespace(data=np.repeat(f[..., None], 3, axis=2).tobytes(), height=480, width=640)
+            for f in frames]
+    corners = [marker_corners(i, K) for i in range(5)]
+    T_vo = vo.robot_curr_position
+    P = K @ np.hstack((np.eye(3), np.zeros((3, 1))))
+    T_ref = np.eye(4)
+    for i in range(1, 5):
+        prev = vo.ros_img_msg_to_opencv_image(msgs[i - 1], "usb_raw")
+        cur = vo.ros_img_msg_to_opencv_image(msgs[i], "usb_raw")
+        np.testing.assert_array_equal(prev, frames[i - 1])
+        T_vo, rel = vo.visual_odometry_calculations(prev, cur, T_vo, corners[i - 1], corners[i])
+        ref = oracle_mod.pair_pose(frames[i - 1], frames[i], K, 500)
+        np.testing.assert_array_equal(vo.essential_matrix, ref["E"])
+        P, T_rel, T_ref = oracle_mod.pose_tail(K, ref["R"], ref["t_unit"], corners[i - 1], corners[i], MARKER_LEN,
+                                               P, T_ref)
+        np.testing.assert_array_equal(vo.previous_projection_matrix, P)
+        np.testing.assert_allclose(rel, T_rel, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(T_vo, T_ref, rtol=0, atol=1e-12)
+    assert len(vo.frame_translations) == 4 and len(vo.projection_matrix_list) == 4
