@@ -190,6 +190,15 @@ GeomArgs stream_geom(dvo_stream* s) {
     g.dist_thresh = c.dist_thresh;
     g.npts = s->buf.npts;
     g.models = s->buf.models;
+    g.nmod = s->buf.nmod;
+    g.cnt = s->buf.rcnt;
+    g.subsets = s->buf.subsets;
+    g.rs = s->buf.rs;
+    g.gscr = s->buf.gscr;
+    g.fprec = s->buf.fprec;
+    g.dk_off = s->buf.dk_off;
+    g.dk_ctl = s->buf.dk_ctl;
+    g.hyp_cap = c.max_iters > 1 ? c.max_iters : 1;
     g.E = s->buf.E;
     g.info = s->buf.info;
     g.Rt = s->buf.Rt;
@@ -225,7 +234,16 @@ int stream_alloc(dvo_stream* s) {
     A(b.nmatch, (size_t)F);
     A(b.pts, (size_t)F * cap * 4);
     A(b.npts, (size_t)F * cap * 4);
-    A(b.models, (size_t)F * kChunk * 90);
+    const size_t hc = (size_t)(s->cfg.max_iters > 1 ? s->cfg.max_iters : 1);
+    A(b.models, (size_t)F * hc * 90);
+    A(b.nmod, (size_t)F * hc);
+    A(b.rcnt, (size_t)F * hc * 10);
+    A(b.subsets, (size_t)F * hc * 5);
+    A(b.rs, (size_t)F);
+    A(b.gscr, (size_t)F * ((hc + 63) / 64) * 200 * 64);
+    A(b.fprec, (size_t)F * ((hc + 63) / 64) * 128 * 64);
+    A(b.dk_off, (size_t)F + 1);
+    A(b.dk_ctl, (size_t)2);
     A(b.status, (size_t)F);
     A(b.E, (size_t)F * 90);
     A(b.info, (size_t)F * 4);
@@ -593,11 +611,17 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     if (!(prob > 0 && prob < 1)) return fail(ctx, DVO_EINVAL, "prob must be in (0, 1)");
     if (m < 5) return fail(ctx, DVO_EFEWPTS, "fewer than 5 correspondences");
     HIP_TRY(hipSetDevice(ctx->device));
-    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask;
+    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *dgs, *drec, *doff, *dctl;
     int rc;
+    const size_t hc = (size_t)(max_iters > 1 ? max_iters : 1);
     if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)m * 32, &dn)) ||
-        (rc = scratch(ctx, 7, (size_t)kChunk * 90 * 8, &dmod)) || (rc = scratch(ctx, 8, 90 * 8, &dE)) ||
-        (rc = scratch(ctx, 9, 16, &dinfo)) || (rc = scratch(ctx, 10, (size_t)m, &dmask)))
+        (rc = scratch(ctx, 7, hc * 90 * 8, &dmod)) || (rc = scratch(ctx, 8, 90 * 8, &dE)) ||
+        (rc = scratch(ctx, 9, 16, &dinfo)) || (rc = scratch(ctx, 10, (size_t)m, &dmask)) ||
+        (rc = scratch(ctx, 16, hc * 4, &dnmod)) || (rc = scratch(ctx, 17, hc * 40, &dcnt)) ||
+        (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
+        (rc = scratch(ctx, 20, ((hc + 63) / 64) * 200 * 64 * 8, &dgs)) ||
+        (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
+        (rc = scratch(ctx, 23, 8, &dctl)))
         return rc;
     GeomArgs g{};
     g.pts_d = (const double*)dpts;
@@ -612,6 +636,15 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.max_iters = max_iters;
     g.npts = (double*)dn;
     g.models = (double*)dmod;
+    g.nmod = (int32_t*)dnmod;
+    g.cnt = (int32_t*)dcnt;
+    g.subsets = (int32_t*)dsub;
+    g.rs = (RansacState*)drs;
+    g.gscr = (double*)dgs;
+    g.fprec = (double*)drec;
+    g.dk_off = (int32_t*)doff;
+    g.dk_ctl = (int32_t*)dctl;
+    g.hyp_cap = (int)hc;
     g.E = (double*)dE;
     g.info = (int32_t*)dinfo;
     g.mask = (uint8_t*)dmask;

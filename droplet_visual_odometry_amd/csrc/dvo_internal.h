@@ -48,6 +48,20 @@ struct Plan {
 };
 
 // Device buffers of one stream (all sized for max_frames).
+// Per-pair RANSAC state carried between the batch-wide round kernels
+// (geometry.hip: sample -> solve -> score -> replay, at most two rounds).
+struct RansacState {
+    uint64_t rng;      // cv::RNG state after the last sampled subset
+    int32_t niters;    // current adaptive iteration bound
+    int32_t iter;      // iterations replayed so far
+    int32_t maxgood;   // best inlier count so far
+    int32_t h0, h1;    // hypotheses sampled in the current round: [h0, h1)
+    int32_t m;         // correspondences
+    int32_t best_h, best_i;  // best model: hypothesis, root
+    int32_t pad[2];
+};
+constexpr int kRansacRound1 = 256;  // hypotheses per pair in round 1
+
 struct Buffers {
     uint8_t* pyr;
     uint8_t* blur;
@@ -68,7 +82,15 @@ struct Buffers {
     int32_t* nmatch;      // [F]
     float* pts;           // [F][kp_cap][4] (x1, y1, x2, y2) KeyPoint_convert pixel coords
     double* npts;         // [F][kp_cap][4] normalised coords for RANSAC / recoverPose
-    double* models;       // [F][kChunk][10][9]
+    double* models;       // [F][hyp_cap][10][9]
+    int32_t* nmod;        // [F][hyp_cap]
+    int32_t* rcnt;        // [F][hyp_cap][10]
+    int32_t* subsets;     // [F][hyp_cap][5]
+    RansacState* rs;      // [F]
+    double* gscr;         // [F][ceil(hyp_cap / 64)][200][64]
+    double* fprec;        // [F][ceil(hyp_cap / 64)][128][64]
+    int32_t* dk_off;      // [F + 1]
+    int32_t* dk_ctl;      // [2]
     int32_t* status;      // [F] per-frame error flags
     double* E;            // [F][90]
     int32_t* info;        // [F][4] rows, inliers, iters, status
@@ -76,7 +98,6 @@ struct Buffers {
     int32_t* good;        // [F]
 };
 
-constexpr int kChunk = 256;   // RANSAC iterations evaluated per round (one per thread)
 
 struct StreamParams {   // passed by value to every batch kernel
     Plan plan;
@@ -116,7 +137,16 @@ struct GeomArgs {
     int max_iters;
     double dist_thresh;
     double* npts;           // [pairs][pts_stride][4] normalised
-    double* models;         // [pairs][kChunk][10][9] scratch
+    double* models;         // [pairs][hyp_cap][10][9] hypothesis models
+    int32_t* nmod;          // [pairs][hyp_cap] models per hypothesis
+    int32_t* cnt;           // [pairs][hyp_cap][10] inlier counts
+    int32_t* subsets;       // [pairs][hyp_cap][5] sampled point indices
+    RansacState* rs;        // [pairs]
+    double* gscr;           // [pairs][ceil(hyp_cap / 64)][200][64] five-point scratch
+    double* fprec;          // [pairs][ceil(hyp_cap / 64)][128][64] five-point records
+    int32_t* dk_off;        // [pairs + 1] round work-list offsets
+    int32_t* dk_ctl;        // [2] queue head, total
+    int hyp_cap;            // max(max_iters, 1)
     double* E;              // [pairs][90]
     int32_t* info;          // [pairs][4] rows, inliers, iters, status
     uint8_t* mask;          // [pairs][pts_stride] findEssentialMat mask, or null

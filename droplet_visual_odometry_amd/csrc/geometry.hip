@@ -25,6 +25,26 @@
 
 namespace dvo {
 
+#ifdef DVO_PROBE
+// Development probe (tools/probe_ransac.py): shader-clock cycles per phase,
+// accumulated by lane 0 of block 0 only.
+__device__ unsigned long long g_probe[32];
+#define PROBE_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime()
+#define PROBE_MARK(i)                                                                 \
+    do {                                                                              \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
+            unsigned long long _n = __builtin_amdgcn_s_memtime();                      \
+            atomicAdd(&g_probe[i], _n - _pt);                                         \
+            _pt = _n;                                                                 \
+        } else {                                                                      \
+            _pt = __builtin_amdgcn_s_memtime();                                       \
+        }                                                                             \
+    } while (0)
+#else
+#define PROBE_DECL
+#define PROBE_MARK(i)
+#endif
+
 struct Cx {
     double re, im;
 };
@@ -61,7 +81,7 @@ __device__ __forceinline__ double dvo_hypot(double a, double b) {
 // lapack.cpp JacobiSVDImpl_ (see oracle/geometry.cpp jacobi_svd); compile-time
 // sizes keep every array in registers.  At has R >= max(N, N1) rows of M.
 template <int M, int N, int N1, int R>
-__device__ void jacobi_svd(double (&At)[R][M], double (&Wout)[N], double (&Vt)[N][N]) {
+__device__ __forceinline__ void jacobi_svd(double (&At)[R][M], double (&Wout)[N], double (&Vt)[N][N]) {
     const double minval = DBL_MIN, eps = DBL_EPSILON * 10;
     double W[N];
 #pragma unroll
@@ -205,134 +225,223 @@ __device__ void jacobi_svd(double (&At)[R][M], double (&Wout)[N], double (&Vt)[N
 }
 
 // ---- Nister coefficient matrix (index tables = oracle PolyTables) ----------
-__device__ constexpr int kLL2Q[4][4] = {{0, 1, 2, 3}, {1, 4, 5, 6}, {2, 5, 7, 8}, {3, 6, 8, 9}};
-__device__ constexpr int kQL2C[10][4] = {{0, 2, 4, 5},   {2, 3, 8, 9},    {4, 8, 10, 11},  {5, 9, 11, 12},
-                                         {3, 1, 6, 7},   {8, 6, 13, 14},  {9, 7, 14, 15},  {10, 13, 16, 17},
-                                         {11, 14, 17, 18}, {12, 15, 18, 19}};
+// Monomial index maps (linear x linear -> quadratic, quadratic x linear ->
+// cubic) as compile-time functions so the unrolled products index registers.
+__host__ __device__ constexpr int ll2q(int i, int j) {
+    return i <= j ? i * 4 - i * (i - 1) / 2 + (j - i) : j * 4 - j * (j - 1) / 2 + (i - j);
+}
+struct QL2C {
+    int v[10][4];
+};
+__host__ __device__ constexpr QL2C make_ql2c() {
+    return QL2C{{{0, 2, 4, 5}, {2, 3, 8, 9}, {4, 8, 10, 11}, {5, 9, 11, 12}, {3, 1, 6, 7}, {8, 6, 13, 14},
+                 {9, 7, 14, 15}, {10, 13, 16, 17}, {11, 14, 17, 18}, {12, 15, 18, 19}}};
+}
+template <int I, int J>
+struct QL2CAt {
+    static constexpr int value = make_ql2c().v[I][J];
+};
+static_assert(ll2q(0, 0) == 0 && ll2q(1, 2) == 5 && ll2q(3, 3) == 9 && ll2q(2, 1) == 5, "ll2q");
+
+template <int I = 0, int J = 0>
+__device__ __forceinline__ void mul_ql_acc(const double* q, const double* l, double* c) {
+    if constexpr (I < 10) {
+        c[QL2CAt<I, J>::value] += q[I] * l[J];
+        if constexpr (J + 1 < 4) mul_ql_acc<I, J + 1>(q, l, c);
+        else mul_ql_acc<I + 1, 0>(q, l, c);
+    }
+}
+template <int I = 0, int J = 0>
+__device__ __forceinline__ void mul_ll_acc(const double* a, const double* b, double* q) {
+    if constexpr (I < 4) {
+        q[ll2q(I, J)] += a[I] * b[J];
+        if constexpr (J + 1 < 4) mul_ll_acc<I, J + 1>(a, b, q);
+        else mul_ll_acc<I + 1, 0>(a, b, q);
+    }
+}
 
 __device__ __forceinline__ void mul_ll(const double* a, const double* b, double* q) {
 #pragma unroll
     for (int k = 0; k < 10; ++k) q[k] = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] += a[i] * b[j];
+    mul_ll_acc(a, b, q);  // (i, j) row-major, as the reference's loops
 }
 __device__ __forceinline__ void mul_ql(const double* q, const double* l, double* c) {
 #pragma unroll
     for (int k = 0; k < 20; ++k) c[k] = 0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += q[i] * l[j];
+    mul_ql_acc(q, l, c);
 }
 
 // Rows: the nine entries of 2 EE^T E - tr(EE^T) E (row-major), then det E;
 // columns 0..9 go to L (the matrix OpenCV inverts), 10..19 to G (its RHS).
-__device__ void coeff_matrix(const double (&EE)[4][9], double* L, double* G) {
-    double E[9][4];
+// Rows of the 10x20 coefficient matrix, L = columns 0..9 and G = 10..19, are
+// written to strided per-thread columns (element k at X[k * 64]): L to LDS, G
+// to global scratch.  The null-space basis EE (4 x 9) is read from LDS
+// (EL[(c * 9 + e) * 64] = EE[c][e]) so the row loops stay rolled; E E^T entries
+// are formed per row block i (the three diagonal ones first, for the trace);
+// recomputed entries are bit-identical.
+__device__ __forceinline__ void ee_entry(const double* EL, int e, double (&o)[4]) {
 #pragma unroll
-    for (int e = 0; e < 9; ++e) {
-        E[e][0] = EE[0][e];
-        E[e][1] = EE[1][e];
-        E[e][2] = EE[2][e];
-        E[e][3] = EE[3][e];
+    for (int c = 0; c < 4; ++c) o[c] = EL[(c * 9 + e) * 64];
+}
+
+__device__ __forceinline__ void eet_entry(const double* EL, int i, int j, double (&o)[10]) {
+    double a[4], b[4], t1[10];
+    ee_entry(EL, i * 3 + 0, a);
+    ee_entry(EL, j * 3 + 0, b);
+    mul_ll(a, b, o);
+#pragma unroll
+    for (int k = 1; k < 3; ++k) {
+        ee_entry(EL, i * 3 + k, a);
+        ee_entry(EL, j * 3 + k, b);
+        mul_ll(a, b, t1);
+#pragma unroll
+        for (int q = 0; q < 10; ++q) o[q] = o[q] + t1[q];
     }
-    double EEt[9][10], t1[10], t2[10];
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double* o = EEt[i * 3 + j];
-            mul_ll(E[i * 3 + 0], E[j * 3 + 0], o);
-            mul_ll(E[i * 3 + 1], E[j * 3 + 1], t1);
-#pragma unroll
-            for (int k = 0; k < 10; ++k) o[k] = o[k] + t1[k];
-            mul_ll(E[i * 3 + 2], E[j * 3 + 2], t1);
-#pragma unroll
-            for (int k = 0; k < 10; ++k) o[k] = o[k] + t1[k];
-        }
+}
+
+__device__ __forceinline__ void coeff_matrix(const double* EL, double* L, double* G) {
     double tr[10];
+    {
+        double d0[10], d1[10], d2[10];
+        eet_entry(EL, 0, 0, d0);
+        eet_entry(EL, 1, 1, d1);
+        eet_entry(EL, 2, 2, d2);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) tr[k] = (EEt[0][k] + EEt[4][k]) + EEt[8][k];
-    double row[20], c1[20], c2[20];
-    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 10; ++k) tr[k] = (d0[k] + d1[k]) + d2[k];
+    }
+    double row[20], c1[20], c2[20], t1[10], t2[10];
+#pragma unroll 1
+    for (int i = 0; i < 3; ++i) {
+        double Ei[3][10];
+        eet_entry(EL, i, 0, Ei[0]);
+        eet_entry(EL, i, 1, Ei[1]);
+        eet_entry(EL, i, 2, Ei[2]);
+#pragma unroll 1
         for (int j = 0; j < 3; ++j) {
-            mul_ql(EEt[i * 3 + 0], E[0 * 3 + j], row);
-            mul_ql(EEt[i * 3 + 1], E[1 * 3 + j], c1);
+            double e0[4], e1[4], e2[4], eij[4];
+            ee_entry(EL, 0 * 3 + j, e0);
+            ee_entry(EL, 1 * 3 + j, e1);
+            ee_entry(EL, 2 * 3 + j, e2);
+            ee_entry(EL, i * 3 + j, eij);
+            mul_ql(Ei[0], e0, row);
+            mul_ql(Ei[1], e1, c1);
 #pragma unroll
             for (int k = 0; k < 20; ++k) row[k] = row[k] + c1[k];
-            mul_ql(EEt[i * 3 + 2], E[2 * 3 + j], c1);
+            mul_ql(Ei[2], e2, c1);
 #pragma unroll
             for (int k = 0; k < 20; ++k) row[k] = row[k] + c1[k];
-            mul_ql(tr, E[i * 3 + j], c1);
+            mul_ql(tr, eij, c1);
             const int r = i * 3 + j;
 #pragma unroll
-            for (int k = 0; k < 10; ++k) L[r * 10 + k] = 2.0 * row[k] - c1[k];
+            for (int k = 0; k < 10; ++k) L[(r * 10 + k) * 64] = 2.0 * row[k] - c1[k];
 #pragma unroll
-            for (int k = 0; k < 10; ++k) G[r * 10 + k] = 2.0 * row[10 + k] - c1[10 + k];
-        }
-    mul_ll(E[4], E[8], t1);
-    mul_ll(E[5], E[7], t2);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
-    mul_ql(t1, E[0], row);
-    mul_ll(E[3], E[8], t1);
-    mul_ll(E[5], E[6], t2);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
-    mul_ql(t1, E[1], c1);
-    mul_ll(E[3], E[7], t1);
-    mul_ll(E[4], E[6], t2);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
-    mul_ql(t1, E[2], c2);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) L[90 + k] = (row[k] - c1[k]) + c2[k];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) G[90 + k] = (row[10 + k] - c1[10 + k]) + c2[10 + k];
-}
-
-// LUImpl<double>(A, 10, b, 10, DBL_EPSILON*100) with dynamic pivoting (scratch).
-__device__ int lu_solve10(double* A, double* b) {
-    const double eps = DBL_EPSILON * 100;
-    const int m = 10, n = 10;
-    int p = 1;
-    for (int i = 0; i < m; i++) {
-        int k = i;
-        for (int j = i + 1; j < m; j++)
-            if (fabs(A[j * m + i]) > fabs(A[k * m + i])) k = j;
-        if (fabs(A[k * m + i]) < eps) return 0;
-        if (k != i) {
-            for (int j = i; j < m; j++) {
-                double t = A[i * m + j];
-                A[i * m + j] = A[k * m + j];
-                A[k * m + j] = t;
-            }
-            for (int j = 0; j < n; j++) {
-                double t = b[i * n + j];
-                b[i * n + j] = b[k * n + j];
-                b[k * n + j] = t;
-            }
-            p = -p;
-        }
-        double d = -1 / A[i * m + i];
-        for (int j = i + 1; j < m; j++) {
-            double alpha = A[j * m + i] * d;
-            for (int c = i + 1; c < m; c++) A[j * m + c] += alpha * A[i * m + c];
-            for (int c = 0; c < n; c++) b[j * n + c] += alpha * b[i * n + c];
+            for (int k = 0; k < 10; ++k) G[(r * 10 + k) * 64] = 2.0 * row[10 + k] - c1[10 + k];
         }
     }
-    for (int i = m - 1; i >= 0; i--)
-        for (int j = 0; j < n; j++) {
-            double s = b[i * n + j];
-            for (int k = i + 1; k < m; k++) s -= A[i * m + k] * b[k * n + j];
-            b[i * n + j] = s / A[i * m + i];
-        }
-    return p;
+    double ea[4], eb[4];
+    auto det2 = [&](int a0, int b0, int a1, int b1) {  // t1 = E[a0] E[b0] - E[a1] E[b1]
+        ee_entry(EL, a0, ea);
+        ee_entry(EL, b0, eb);
+        mul_ll(ea, eb, t1);
+        ee_entry(EL, a1, ea);
+        ee_entry(EL, b1, eb);
+        mul_ll(ea, eb, t2);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) t1[k] = t1[k] - t2[k];
+    };
+    det2(4, 8, 5, 7);
+    ee_entry(EL, 0, ea);
+    mul_ql(t1, ea, row);
+    det2(3, 8, 5, 6);
+    ee_entry(EL, 1, ea);
+    mul_ql(t1, ea, c1);
+    det2(3, 7, 4, 6);
+    ee_entry(EL, 2, ea);
+    mul_ql(t1, ea, c2);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L[(90 + k) * 64] = (row[k] - c1[k]) + c2[k];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) G[(90 + k) * 64] = (row[10 + k] - c1[10 + k]) + c2[10 + k];
 }
 
-__device__ int solve_cubic(const double* c, double* x) {
+// LUImpl<double>(A, 10, b, 10, DBL_EPSILON*100) (matrix_decomp.cpp), split so
+// the 10x10 A stays in registers: the factorisation records the pivot rows and
+// keeps each elimination multiplier in A's (never again read) lower triangle;
+// the right-hand side is then replayed one column at a time from LDS with the
+// identical operation sequence.  Only solution rows 4..9 are consumed by the
+// five-point solver and back substitution of row i reads rows > i only, so
+// rows 0..3 are not back-substituted.
+__device__ __forceinline__ bool lu10_factor(double (&A)[10][10], int (&piv)[10]) {
+    const double eps = DBL_EPSILON * 100;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        int k = i;
+        double amax = fabs(A[i][i]);
+#pragma unroll
+        for (int j = i + 1; j < 10; j++) {
+            const double v = fabs(A[j][i]);
+            if (v > amax) {
+                k = j;
+                amax = v;
+            }
+        }
+        if (amax < eps) return false;
+        piv[i] = k;
+#pragma unroll
+        for (int r = i + 1; r < 10; r++)
+            if (r == k) {
+#pragma unroll
+                for (int j = i; j < 10; j++) {
+                    const double t = A[i][j];
+                    A[i][j] = A[r][j];
+                    A[r][j] = t;
+                }
+            }
+        const double d = -1 / A[i][i];
+#pragma unroll
+        for (int j = i + 1; j < 10; j++) {
+            const double alpha = A[j][i] * d;
+            A[j][i] = alpha;
+#pragma unroll
+            for (int c = i + 1; c < 10; c++) A[j][c] += alpha * A[i][c];
+        }
+    }
+    return true;
+}
+
+// Gin: right-hand side (strided column, element k at Gin[k * 64]); solution
+// rows 4..9 go to X with the same layout.
+__device__ __forceinline__ void lu10_solve_cols(const double (&A)[10][10], const int (&piv)[10], const double* Gin, double* X) {
+    for (int c = 0; c < 10; c++) {
+        double x[10];
+#pragma unroll
+        for (int r = 0; r < 10; r++) x[r] = Gin[(r * 10 + c) * 64];
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const int k = piv[i];
+#pragma unroll
+            for (int r = i + 1; r < 10; r++)
+                if (r == k) {
+                    const double t = x[i];
+                    x[i] = x[r];
+                    x[r] = t;
+                }
+#pragma unroll
+            for (int j = i + 1; j < 10; j++) x[j] += A[j][i] * x[i];
+        }
+#pragma unroll
+        for (int i = 9; i >= 4; i--) {
+            double sacc = x[i];
+#pragma unroll
+            for (int k = i + 1; k < 10; k++) sacc -= A[i][k] * x[k];
+            x[i] = sacc / A[i][i];
+        }
+#pragma unroll
+        for (int r = 4; r < 10; r++) X[(r * 10 + c) * 64] = x[r];
+    }
+}
+
+__device__ __forceinline__ int solve_cubic(const double* c, double* x) {
     double a0 = c[0], a1 = c[1], a2 = c[2], a3 = c[3];
     double x0 = 0, x1 = 0, x2 = 0;
     int n;
@@ -401,7 +510,7 @@ __device__ int solve_cubic(const double* c, double* x) {
     return n;
 }
 
-__device__ Cx same_root_step(Cx num, int num_same_root) {
+__device__ __forceinline__ Cx same_root_step(Cx num, int num_same_root) {
     double ore = num.re, oim = num.im;
     int sq_times = num_same_root % 2 == 0 ? num_same_root / 2 : num_same_root / 2 - 1;
     for (int j = 0; j < sq_times; j++) {
@@ -430,43 +539,127 @@ __device__ Cx same_root_step(Cx num, int num_same_root) {
 }
 
 // solvePoly, full degree 10: constant indices keep roots/coeffs in registers.
-__device__ void solve_poly10(const double (&rc)[11], Cx (&roots)[10]) {
-    Cx coeffs[11];
+// One Gauss-Seidel sweep of solvePoly's Durand-Kerner iteration (mathfuncs.cpp)
+// over the 10 roots; `moved` is the reference's maxDiff > 0.  kSameRoot=false
+// leaves out the (register-hungry) coincident-root step and only reports it in
+// `same`; the caller then redoes the polynomial with kSameRoot=true.
+template <bool kSameRoot>
+__device__ __forceinline__ void dk_sweep(const double (&c)[11], Cx (&roots)[10], bool& moved, bool& same) {
+    moved = false;
 #pragma unroll
-    for (int i = 0; i <= 10; i++) coeffs[i] = Cx{rc[i], 0};
+    for (int i = 0; i < 10; i++) {
+        const Cx p = roots[i];
+        Cx num{c[10], 0}, denom{c[10], 0};
+        int num_same_root = 1;
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+            const Cx t = cmul(num, p);
+            num = Cx{t.re + c[10 - j - 1], t.im + 0.0};
+            if (j != i) {
+                Cx d = csub(p, roots[j]);
+                if (d.re == 0 && d.im == 0) num_same_root++;
+                else denom = cmul(denom, d);
+            }
+        }
+        num = cdiv(num, denom);
+        if constexpr (kSameRoot) {
+            if (num_same_root > 1) num = same_root_step(num, num_same_root);
+        } else {
+            same |= num_same_root > 1;
+        }
+        roots[i] = csub(p, num);
+        // std::max(maxDiff, cv::abs(num)) > 0  <=>  re^2 + im^2 > 0 (sqrt is monotone, NaN stays out)
+        moved |= (num.re * num.re + num.im * num.im) > 0;
+    }
+}
+
+__device__ __forceinline__ void dk_init(Cx (&roots)[10]) {
     Cx p{1, 0}, r{1, 1};
 #pragma unroll
     for (int i = 0; i < 10; i++) {
         roots[i] = p;
         p = cmul(p, r);
     }
-    for (int iter = 0; iter < 300; iter++) {
-        double maxDiff = 0;
+}
+
+__device__ __forceinline__ bool dk_same(const Cx (&a)[10], const Cx (&b)[10]) {
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 10; i++)
+        eq &= (__double_as_longlong(a[i].re) == __double_as_longlong(b[i].re)) &
+              (__double_as_longlong(a[i].im) == __double_as_longlong(b[i].im));
+    return eq;
+}
+
+// Brent cycle detection on the sweep's state.  The sweep is a deterministic map
+// S_k -> S_{k+1} of the 10 roots, so once S_k == S_a (a < k) the sequence is
+// periodic with period k - a and S_300 = S_{k + (300 - k) mod (k - a)}: the
+// iteration stops at that sweep with the roots the reference's 300 sweeps end
+// on (or earlier at the reference's own maxDiff <= 0 exit).
+// `saved` is a strided per-lane column (element k at saved[k * stride]) so the
+// snapshot can live in LDS in the persistent kernel.
+struct DkBrent {
+    double* saved;
+    int stride;
+    int it, saved_it, power, target;
+    __device__ void snap(const Cx (&roots)[10]) {
 #pragma unroll
         for (int i = 0; i < 10; i++) {
-            p = roots[i];
-            Cx num = coeffs[10], denom = coeffs[10];
-            int num_same_root = 1;
-#pragma unroll
-            for (int j = 0; j < 10; j++) {
-                num = cadd(cmul(num, p), coeffs[10 - j - 1]);
-                if (j != i) {
-                    Cx d = csub(p, roots[j]);
-                    if (d.re == 0 && d.im == 0) num_same_root++;
-                    else denom = cmul(denom, d);
-                }
-            }
-            num = cdiv(num, denom);
-            if (num_same_root > 1) num = same_root_step(num, num_same_root);
-            roots[i] = csub(p, num);
-            const double an = cabs_(num);
-            maxDiff = maxDiff < an ? an : maxDiff;  // std::max(maxDiff, cv::abs(num))
+            saved[(2 * i) * stride] = roots[i].re;
+            saved[(2 * i + 1) * stride] = roots[i].im;
         }
-        if (maxDiff <= 0) break;
     }
+    __device__ void start(const Cx (&roots)[10]) {
+        snap(roots);
+        it = 0;
+        saved_it = 0;
+        power = 1;
+        target = 300;
+    }
+    // after one sweep; true when the roots are final
+    __device__ bool step(const Cx (&roots)[10], bool moved) {
+        ++it;
+        if (!moved || it >= target) return true;
+        if (target == 300) {
+            bool eq = true;
+#pragma unroll
+            for (int i = 0; i < 10; i++)
+                eq &= (__double_as_longlong(roots[i].re) == __double_as_longlong(saved[(2 * i) * stride])) &
+                      (__double_as_longlong(roots[i].im) == __double_as_longlong(saved[(2 * i + 1) * stride]));
+            if (eq) {
+                target = it + (300 - it) % (it - saved_it);
+                return it >= target;
+            }
+            if (it - saved_it == power) {
+                snap(roots);
+                saved_it = it;
+                power <<= 1;
+            }
+        }
+        return false;
+    }
+};
+
+__device__ __forceinline__ void dk_finish(Cx (&roots)[10]) {
 #pragma unroll
     for (int i = 0; i < 10; i++)
         if (fabs(roots[i].im) < 1e-100) roots[i].im = 0;
+}
+
+// solvePoly for a degree-10 polynomial (single thread).
+__device__ __forceinline__ void solve_poly10(const double (&c)[11], Cx (&roots)[10]) {
+    dk_init(roots);
+    double saved[20];
+    DkBrent br;
+    br.saved = saved;
+    br.stride = 1;
+    br.start(roots);
+    for (;;) {
+        bool moved, same = false;
+        dk_sweep<true>(c, roots, moved, same);
+        if (br.step(roots, moved)) break;
+    }
+    dk_finish(roots);
 }
 
 // solvePoly generic (leading coefficients trimmed; rare): scratch arrays.
@@ -508,7 +701,7 @@ __device__ int solve_poly_generic(const double* rc, int n0, Cx* roots) {
     return n;
 }
 
-__device__ void poly_mul(const double* a, int na, const double* b, int nb, double* r) {
+__device__ __forceinline__ void poly_mul(const double* a, int na, const double* b, int nb, double* r) {
 #pragma unroll
     for (int k = 0; k < na + nb - 1; ++k) r[k] = 0;
 #pragma unroll
@@ -519,7 +712,23 @@ __device__ void poly_mul(const double* a, int na, const double* b, int nb, doubl
 
 // five-point.cpp EMEstimatorCallback::runKernel; q: 5 x (x1, y1, x2, y2)
 // normalised.  Writes up to 10 models (9 doubles each) and returns the count.
-__device__ int five_point(const double (&q)[5][4], double* models) {
+// Five-point solver (five-point.cpp, Nister via Stewenius' coefficient matrix)
+// in three stages so the Durand-Kerner root finder can run as its own
+// load-balanced kernel.  A hypothesis record R holds, element k at R[k * 64]:
+//   [0, 11) polynomial coefficients c, [11, 50) the 3 x 13 matrix b,
+//   [50, 86) the null-space basis EE (4 x 9), [86, 106) roots (re, im),
+//   106: number of roots, 107: 1 when c[10] is negligible (generic solvePoly),
+//   2 when two roots coincided exactly in the fast Durand-Kerner kernel.
+constexpr int kRecC = 0, kRecB = 11, kRecEE = 50, kRecRoots = 86, kRecNr = 106, kRecGeneric = 107;
+constexpr int kRecDoubles = 128;
+
+// Stage A: Q -> null space (JacobiSVD) -> 10x20 coefficient matrix -> LU solve
+// -> b -> degree-10 polynomial.  EL: this thread's LDS column of 36 doubles;
+// Gg: its global scratch column of 200 doubles ([0, 100) L, [100, 200) G,
+// overwritten in place by the solution rows 4..9).
+__device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, double* Gg, double* R) {
+    double* const G = Gg + 100 * 64;
+    PROBE_DECL;
     double At[9][9], W[5], Vt[5][5];
 #pragma unroll
     for (int i = 0; i < 9; ++i)
@@ -538,42 +747,60 @@ __device__ int five_point(const double (&q)[5][4], double* models) {
         At[i][7] = y1 + 0.0;
         At[i][8] = 1.0;
     }
+    PROBE_MARK(10);
     jacobi_svd<9, 5, 9, 9>(At, W, Vt);
-    double EE[4][9];
+    PROBE_MARK(11);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int k = 0; k < 9; ++k) EE[r][k] = At[5 + r][k] + 0.0;
+        for (int k = 0; k < 9; ++k) {
+            const double v = At[5 + r][k] + 0.0;
+            EL[(r * 9 + k) * 64] = v;
+            R[(kRecEE + r * 9 + k) * 64] = v;
+        }
     double b[3 * 13];
     {
         // A = A.colRange(0,10).inv() * A.colRange(10,20) == solve(A1, A2, DECOMP_LU)
-        double L[100], G[100];
-        coeff_matrix(EE, L, G);
-        if (!lu_solve10(L, G))
-            for (int k = 0; k < 100; ++k) G[k] = 0;
+        double L[10][10];
+        int piv[10];
+        coeff_matrix(EL, Gg, G);
+#pragma unroll
+        for (int r = 0; r < 10; ++r)
+#pragma unroll
+            for (int k = 0; k < 10; ++k) L[r][k] = Gg[(r * 10 + k) * 64];
+        PROBE_MARK(12);
+        if (lu10_factor(L, piv)) {
+            lu10_solve_cols(L, piv, G, G);
+        } else {
+#pragma unroll
+            for (int k = 40; k < 100; ++k) G[k * 64] = 0;
+        }
+        PROBE_MARK(13);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double* a1 = G + (i * 2 + 4) * 10;
-            const double* a2 = G + (i * 2 + 5) * 10;
+            const double* a1 = G + (i * 2 + 4) * 10 * 64;
+            const double* a2 = G + (i * 2 + 5) * 10 * 64;
             double row1[13], row2[13];
 #pragma unroll
             for (int k = 0; k < 13; ++k) row1[k] = row2[k] = 0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row1[1 + k] = (a1[k] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row1[1 + k] = (a1[k * 64] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row1[5 + k] = (a1[3 + k] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row1[5 + k] = (a1[(3 + k) * 64] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) row1[9 + k] = (a1[6 + k] + 0.0) + 0.0;
+            for (int k = 0; k < 4; ++k) row1[9 + k] = (a1[(6 + k) * 64] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row2[0 + k] = (a2[k] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row2[0 + k] = (a2[k * 64] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row2[4 + k] = (a2[3 + k] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row2[4 + k] = (a2[(3 + k) * 64] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) row2[8 + k] = (a2[6 + k] + 0.0) + 0.0;
+            for (int k = 0; k < 4; ++k) row2[8 + k] = (a2[(6 + k) * 64] + 0.0) + 0.0;
 #pragma unroll
             for (int k = 0; k < 13; ++k) b[i * 13 + k] = row1[k] - row2[k];
         }
     }
+#pragma unroll
+    for (int k = 0; k < 39; ++k) R[(kRecB + k) * 64] = b[k];
     double px[3][4], py[3][4], pc[3][5];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -584,7 +811,7 @@ __device__ int five_point(const double (&q)[5][4], double* models) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) pc[j][k] = b[j * 13 + 12 - k];
     }
-    double u[8], v[8], m1[8], m2[8], m3[8], t1[11], t2[11], t3[11], c[11];
+    double u[8], v[8], m1[8], m2[8], m3[8], t1[11], t2[11], t3[11];
     poly_mul(py[1], 4, pc[2], 5, u);
     poly_mul(pc[1], 5, py[2], 4, v);
 #pragma unroll
@@ -600,20 +827,51 @@ __device__ int five_point(const double (&q)[5][4], double* models) {
     poly_mul(px[0], 4, m1, 8, t1);
     poly_mul(py[0], 4, m2, 8, t2);
     poly_mul(pc[0], 5, m3, 7, t3);
+    double c10 = 0;
 #pragma unroll
-    for (int k = 0; k < 11; ++k) c[k] = (t1[k] - t2[k]) + t3[k];
-
-    Cx roots[10];
-    int nr = 10;
-    if (fabs(c[10]) > DBL_EPSILON) {
-        solve_poly10(c, roots);
-    } else {
-        nr = solve_poly_generic(c, 10, roots);
+    for (int k = 0; k < 11; ++k) {
+        const double ck = (t1[k] - t2[k]) + t3[k];
+        R[(kRecC + k) * 64] = ck;
+        c10 = ck;
     }
+    R[kRecGeneric * 64] = fabs(c10) > DBL_EPSILON ? 0.0 : 1.0;
+    PROBE_MARK(14);
+}
+
+// Stage C: roots -> (x, y, z) by the 3x3 null space of B(z) -> E, normalised.
+// Polynomials flagged generic (leading coefficient negligible) are solved here.
+__device__ __forceinline__ void dk_store(double* R, Cx (&roots)[10]);
+__device__ __forceinline__ int fp_stage_c(double* R, double* models) {
+    PROBE_DECL;
+    if (R[kRecGeneric * 64] == 2.0) {
+        double c[11];
+        Cx roots[10];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
+        solve_poly10(c, roots);
+        dk_store(R, roots);
+    } else if (R[kRecGeneric * 64] != 0.0) {
+        double c[11];
+        Cx roots[10];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
+        const int nr = solve_poly_generic(c, 10, roots);
+        for (int i = 0; i < nr; ++i) {
+            R[(kRecRoots + 2 * i) * 64] = roots[i].re;
+            R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
+        }
+        R[kRecNr * 64] = nr;
+    }
+    double b[39], EE[36];
+#pragma unroll
+    for (int k = 0; k < 39; ++k) b[k] = R[(kRecB + k) * 64];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) EE[k] = R[(kRecEE + k) * 64];
+    const int nr = (int)R[kRecNr * 64];
     int count = 0;
     for (int i = 0; i < nr; ++i) {
-        if (fabs(roots[i].im) > 1e-10) continue;
-        double z1 = roots[i].re, z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+        if (fabs(R[(kRecRoots + 2 * i + 1) * 64]) > 1e-10) continue;
+        double z1 = R[(kRecRoots + 2 * i) * 64], z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
         double bz[3][3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -632,7 +890,7 @@ __device__ int five_point(const double (&q)[5][4], double* models) {
         double xs = vt3[2][0] / vt3[2][2], ys = vt3[2][1] / vt3[2][2];
         double e[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) e[k] = (((EE[0][k] * xs + EE[1][k] * ys) + 0.0) + EE[2][k] * z1) + EE[3][k];
+        for (int k = 0; k < 9; ++k) e[k] = (((EE[k] * xs + EE[9 + k] * ys) + 0.0) + EE[18 + k] * z1) + EE[27 + k];
         double s = 0;
         s += e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3];
         s += e[4] * e[4] + e[5] * e[5] + e[6] * e[6] + e[7] * e[7];
@@ -643,7 +901,32 @@ __device__ int five_point(const double (&q)[5][4], double* models) {
         for (int k = 0; k < 9; ++k) out[k] = e[k] * inv_n + 0.0;
         count++;
     }
+    PROBE_MARK(16);
     return count;
+}
+
+__device__ __forceinline__ void dk_store(double* R, Cx (&roots)[10]) {
+    dk_finish(roots);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        R[(kRecRoots + 2 * i) * 64] = roots[i].re;
+        R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
+    }
+    R[kRecNr * 64] = 10;
+}
+
+// All three stages in one thread (test hook).  R: a 128-double record column.
+__device__ __forceinline__ int five_point(const double (&q)[5][4], double* models, double* EL, double* Gg, double* R) {
+    fp_stage_a(q, EL, Gg, R);
+    if (R[kRecGeneric * 64] == 0.0) {
+        double c[11];
+        Cx roots[10];
+#pragma unroll
+        for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
+        solve_poly10(c, roots);
+        dk_store(R, roots);
+    }
+    return fp_stage_c(R, models);
 }
 
 __device__ __forceinline__ float sampson_err(const double* E, double x1, double y1, double x2, double y2) {
@@ -701,158 +984,359 @@ __global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
     }
 }
 
-constexpr int kRNT = 256;
+// ---- findEssentialMat RANSAC (ptsetreg.cpp RANSACPointSetRegistrator::run) ----
+// The sequential loop "sample 5 -> five-point -> count inliers of each root ->
+// keep the first model beating max(best, 4) and shrink niters" is split into
+// batch-wide kernels.  Hypotheses only depend on the RNG stream, so a round
+// samples a range of them (one thread per pair, sequential RNG), solves all of
+// them in parallel (one thread per hypothesis), counts inliers of every root
+// in parallel (one wave per model), then replays the sequential bookkeeping in
+// order (one thread per pair).  niters never grows, so round 1 covers
+// [0, min(256, niters)) and round 2 everything left, [256, niters): the result
+// is the sequential loop's, bit for bit.
+constexpr int kSolveNT = 64;
+constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = 1024;
 
-__global__ __launch_bounds__(kRNT) void ransac_kernel(GeomArgs g) {
-    const int p = blockIdx.x;
-    const int m = pair_m(g, p);
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
-    double* E_out = g.E + (int64_t)p * 90;
-    int32_t* info = g.info + (int64_t)p * 4;
-    double* models = g.models + (int64_t)p * kChunk * 90;
-    __shared__ int s_idx[kChunk][5];
-    __shared__ int s_nmod[kChunk];
-    __shared__ int s_pref[kChunk + 1];
-    __shared__ int s_cnt[kChunk * 10];
-    __shared__ double s_best[9];
-    __shared__ uint64_t s_rng;
-    __shared__ int s_niters, s_iter, s_maxgood, s_done;
-    if (m < 5) {
-        if (tid == 0) {
-            info[0] = 0;
-            info[1] = 0;
-            info[2] = 0;
-            info[3] = DVO_EFEWPTS;
+__global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= pairs) return;
+    RansacState S = g.rs[p];
+    int32_t* idx = g.subsets + (int64_t)p * g.hyp_cap * 5;
+    int h0, h1;
+    if (round == 0) {
+        S.m = pair_m(g, p);
+        S.rng = ~0ull;  // RNG rng((uint64)-1)
+        S.niters = g.max_iters > 1 ? g.max_iters : 1;
+        S.iter = 0;
+        S.maxgood = 0;
+        S.best_h = S.best_i = -1;
+        h0 = 0;
+        if (S.m < 5) {
+            h1 = 0;
+        } else if (S.m == 5) {  // count == modelPoints: one direct solve, no RANSAC
+            for (int i = 0; i < 5; ++i) idx[i] = i;
+            h1 = 1;
+        } else {
+            h1 = min(kRansacRound1, S.niters);
         }
-        return;
-    }
-    const double thr = g.threshold / ((g.fx + g.fy) / 2);
-    const float t = (float)(thr * thr);
-    if (m == 5) {
-        if (tid == 0) {
-            double q[5][4];
-            for (int i = 0; i < 5; ++i)
-                for (int k = 0; k < 4; ++k) q[i][k] = npts[i * 4 + k];
-            int k = five_point(q, E_out);
-            info[0] = 3 * k;
-            info[1] = k > 0 ? 5 : 0;
-            info[2] = 1;
-            info[3] = k > 0 ? DVO_OK : DVO_ENOMODEL;
-            if (g.mask && k > 0)
-                for (int i = 0; i < 5; ++i) g.mask[(int64_t)p * g.pts_stride + i] = 1;
+        if (S.m <= 5) {
+            S.h0 = h0;
+            S.h1 = h1;
+            g.rs[p] = S;
+            return;
         }
-        return;
+    } else {
+        h0 = S.h1;
+        h1 = (S.m > 5 && S.iter < S.niters) ? S.niters : h0;
     }
-    if (tid == 0) {
-        s_rng = ~0ull;
-        s_niters = g.max_iters > 1 ? g.max_iters : 1;
-        s_iter = 0;
-        s_maxgood = 0;
-        s_done = 0;
+    const unsigned m = (unsigned)S.m;
+    Rng rng{S.rng};
+    for (int h = h0; h < h1; ++h) {  // getSubset: 5 distinct indices, rng.uniform(0, count)
+        int v[5];
+        for (int i = 0; i < 5; ++i) {
+            for (;;) {
+                v[i] = (int)(rng.next() % m);
+                bool dup = false;
+                for (int j = 0; j < i; ++j) dup |= v[j] == v[i];
+                if (!dup) break;
+            }
+            idx[(int64_t)h * 5 + i] = v[i];
+        }
+    }
+    S.rng = rng.state;
+    S.h0 = h0;
+    S.h1 = h1;
+    g.rs[p] = S;
+}
+
+__device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
+    const int nblk = (g.hyp_cap + 63) >> 6;
+    return g.fprec + ((int64_t)(p * nblk + (h >> 6)) * kRecDoubles) * 64 + (h & 63);
+}
+
+// Work list of the round for the Durand-Kerner kernel: exclusive prefix of the
+// per-pair hypothesis counts, the total, and a reset queue head.
+__global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs) {
+    __shared__ int s_sum[1024];
+    __shared__ int s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    for (int b0 = 0; b0 < pairs; b0 += 1024) {
+        const int p = b0 + threadIdx.x;
+        const int n = p < pairs ? max(0, g.rs[p].h1 - g.rs[p].h0) : 0;
+        __syncthreads();
+        s_sum[threadIdx.x] = n;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+            const int v = threadIdx.x >= off ? s_sum[threadIdx.x - off] : 0;
+            __syncthreads();
+            s_sum[threadIdx.x] += v;
+            __syncthreads();
+        }
+        if (p < pairs) g.dk_off[p] = s_carry + s_sum[threadIdx.x] - n;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry += s_sum[1023];
     }
     __syncthreads();
-    while (true) {
-        const int iter0 = s_iter, niters0 = s_niters;
-        if (s_done || iter0 >= niters0) break;
-        const int C = min(kChunk, niters0 - iter0);
-        if (tid == 0) {  // getSubset for C consecutive iterations
-            Rng rng{s_rng};
-            for (int h = 0; h < C; ++h)
-                for (int i = 0; i < 5; ++i) {
-                    int v;
-                    for (;;) {
-                        v = (int)(rng.next() % (unsigned)m);
-                        int j;
-                        for (j = 0; j < i; ++j)
-                            if (s_idx[h][j] == v) break;
-                        if (j == i) break;
-                    }
-                    s_idx[h][i] = v;
-                }
-            s_rng = rng.state;
-        }
-        __syncthreads();
-        if (tid < C) {
-            double q[5][4];
+    if (threadIdx.x == 0) {
+        g.dk_off[pairs] = s_carry;
+        g.dk_ctl[0] = 0;
+        g.dk_ctl[1] = s_carry;
+    }
+}
+
+// Stage A of every hypothesis of the round (one thread each).
+__global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    const RansacState& S = g.rs[p];
+    const int h0 = S.h0, h1 = S.h1;
+    const int h = h0 + blockIdx.x * kSolveNT + threadIdx.x;
+    if (h0 + (int)blockIdx.x * kSolveNT >= h1) return;
+    __shared__ double lds_g[36 * kSolveNT];
+    if (h >= h1) return;
+    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
+    const int32_t* idx = g.subsets + ((int64_t)p * g.hyp_cap + h) * 5;
+    double q[5][4];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                const double* src = npts + (int64_t)s_idx[tid][i] * 4;
+    for (int i = 0; i < 5; ++i) {
+        const double* src = npts + (int64_t)idx[i] * 4;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) q[i][k] = src[k];
-            }
-            s_nmod[tid] = five_point(q, models + (int64_t)tid * 90);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int s = 0;
-            for (int h = 0; h < C; ++h) {
-                s_pref[h] = s;
-                s += s_nmod[h];
-            }
-            s_pref[C] = s;
-        }
-        __syncthreads();
-        // score every model of the round: one wave per model, lanes over points
-        const int T = s_pref[C];
-        for (int e = wid; e < T; e += kRNT / 64) {
-            int lo = 0, hi = C - 1;  // h with s_pref[h] <= e < s_pref[h+1]
+        for (int k = 0; k < 4; ++k) q[i][k] = src[k];
+    }
+    double* gg = g.gscr + ((int64_t)p * gridDim.x + blockIdx.x) * 200 * kSolveNT + threadIdx.x;
+    fp_stage_a(q, lds_g + threadIdx.x, gg, hyp_record(g, p, h));
+}
+
+// Durand-Kerner for every polynomial of the round: persistent lanes pull
+// polynomials from a queue, so a lane whose roots settle early (Brent) takes
+// the next one instead of idling until the slowest lane of its wave is done.
+constexpr int kDkNT = 256, kDkBlocks = 1024;
+__global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8))) void ransac_dk_kernel(GeomArgs g, int pairs) {
+    const int total = g.dk_ctl[1];
+    if ((int)blockIdx.x * kDkNT >= total) return;
+    __shared__ double s_saved[20 * kDkNT];
+    int item = -1;
+    double c[11];
+    Cx roots[10];
+    DkBrent br;
+    br.saved = s_saved + threadIdx.x;
+    br.stride = kDkNT;
+    double* R = nullptr;
+    for (;;) {
+        while (item < 0) {
+            item = atomicAdd(&g.dk_ctl[0], 1);
+            if (item >= total) break;
+            int lo = 0, hi = pairs - 1;  // pair p with off[p] <= item < off[p + 1]
             while (lo < hi) {
-                int mid = (lo + hi + 1) >> 1;
-                if (s_pref[mid] <= e) lo = mid;
+                const int mid = (lo + hi + 1) >> 1;
+                if (g.dk_off[mid] <= item) lo = mid;
                 else hi = mid - 1;
             }
-            const int h = lo, i = e - s_pref[h];
-            const double* Em = models + (int64_t)h * 90 + i * 9;
+            R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
+            if (R[kRecGeneric * 64] != 0.0) {  // stage C runs the generic solver
+                item = -1;
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
+            dk_init(roots);
+            br.start(roots);
+        }
+        const bool active = item >= 0 && item < total;
+        if (__ballot(active) == 0) break;
+        if (active) {
+            bool moved, same = false;
+            dk_sweep<false>(c, roots, moved, same);
+            if (same) {  // coincident roots: stage C redoes this polynomial exactly
+                R[kRecGeneric * 64] = 2.0;
+                item = -1;
+            } else if (br.step(roots, moved)) {
+                dk_store(R, roots);
+                item = -1;
+            }
+        }
+    }
+}
+
+// Stage C of every hypothesis of the round: models and their count.
+__global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    const RansacState& S = g.rs[p];
+    const int h0 = S.h0, h1 = S.h1;
+    const int h = h0 + blockIdx.x * kSolveNT + threadIdx.x;
+    if (h >= h1) return;
+    g.nmod[(int64_t)p * g.hyp_cap + h] =
+        fp_stage_c(hyp_record(g, p, h), g.models + ((int64_t)p * g.hyp_cap + h) * 90);
+}
+
+// Inlier counts of every root of kScoreHyps hypotheses of one pair; the pair's
+// normalised points stream through LDS in chunks, one wave per model.
+__global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    const RansacState& S = g.rs[p];
+    const int hb = S.h0 + blockIdx.x * kScoreHyps;
+    if (hb >= S.h1 || S.m <= 5) return;
+    const int hn = min(kScoreHyps, S.h1 - hb);
+    const int m = S.m;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ double s_pts[kScoreChunk * 4];
+    __shared__ double s_E[kScoreHyps * 10 * 9];
+    __shared__ int s_pref[kScoreHyps + 1];
+    __shared__ int s_cnt[kScoreHyps * 10];
+    const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
+    if (tid == 0) {
+        int acc = 0;
+        for (int i = 0; i < hn; ++i) {
+            s_pref[i] = acc;
+            acc += g.nmod[hbase + i];
+        }
+        s_pref[hn] = acc;
+    }
+    __syncthreads();
+    const int T = s_pref[hn];
+    for (int e = tid; e < T * 9; e += kScoreNT) {
+        const int mi = e / 9, k = e - mi * 9;
+        int h = 0;
+        while (h + 1 < hn && s_pref[h + 1] <= mi) ++h;
+        s_E[e] = g.models[(hbase + h) * 90 + (mi - s_pref[h]) * 9 + k];
+    }
+    for (int e = tid; e < T; e += kScoreNT) s_cnt[e] = 0;
+    const double thr = g.threshold / ((g.fx + g.fy) / 2);
+    const float t = (float)(thr * thr);
+    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
+    for (int c0 = 0; c0 < m; c0 += kScoreChunk) {
+        const int cn = min(kScoreChunk, m - c0);
+        __syncthreads();
+        for (int e = tid; e < cn * 4; e += kScoreNT) s_pts[e] = npts[(int64_t)c0 * 4 + e];
+        __syncthreads();
+        for (int e = wid; e < T; e += kScoreNT / 64) {
             double Ed[9];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) Ed[k] = Em[k];
+            for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
             int cnt = 0;
-            for (int j = lane; j < m; j += 64) {
-                const double* pt = npts + (int64_t)j * 4;
-                float err = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]);
+            for (int j = lane; j < cn; j += 64) {
+                const double* pt = s_pts + j * 4;
+                const float err = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]);
                 cnt += __popcll(__ballot(err <= t));
             }
-            if (lane == 0) s_cnt[h * 10 + i] = cnt;
+            if (lane == 0) s_cnt[e] += cnt;
         }
+    }
+    __syncthreads();
+    for (int e = tid; e < T; e += kScoreNT) {
+        int h = 0;
+        while (h + 1 < hn && s_pref[h + 1] <= e) ++h;
+        g.cnt[(hbase + h) * 10 + (e - s_pref[h])] = s_cnt[e];
+    }
+}
+
+// The sequential bookkeeping of RANSACPointSetRegistrator::run over this
+// round's hypotheses, in order (counts staged through LDS, thread 0 replays).
+constexpr int kReplayNT = 64, kReplayMax = 1024;
+__global__ __launch_bounds__(kReplayNT) void ransac_replay_kernel(GeomArgs g) {
+    const int p = blockIdx.x;
+    RansacState* Sp = g.rs + p;
+    const int h0 = Sp->h0, h1 = Sp->h1;
+    if (Sp->m <= 5 || h1 <= h0) return;
+    __shared__ int s_nmod[kReplayMax];
+    __shared__ int s_cnt[kReplayMax * 10];
+    const int64_t base = (int64_t)p * g.hyp_cap;
+    for (int h0c = h0; h0c < h1; h0c += kReplayMax) {  // hyp_cap > kReplayMax: chunked
+        const int hn = min(kReplayMax, h1 - h0c);
         __syncthreads();
-        if (tid == 0) {  // RANSACPointSetRegistrator::run, sequential replay
-            int niters = s_niters, maxgood = s_maxgood, it = iter0;
-            for (int h = 0; h < C; ++h, ++it) {
-                if (it >= niters) break;
+        for (int e = threadIdx.x; e < hn; e += kReplayNT) s_nmod[e] = g.nmod[base + h0c + e];
+        for (int e = threadIdx.x; e < hn * 10; e += kReplayNT) s_cnt[e] = g.cnt[(base + h0c) * 10 + e];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            RansacState S = *Sp;
+            const int m = S.m;
+            int it = S.iter, niters = S.niters, maxgood = S.maxgood;
+            for (int h = 0; h < hn && it < niters; ++h, ++it) {
                 for (int i = 0; i < s_nmod[h]; ++i) {
-                    int good = s_cnt[h * 10 + i];
+                    const int good = s_cnt[h * 10 + i];
                     if (good > (maxgood > 4 ? maxgood : 4)) {
-                        const double* Em = models + (int64_t)h * 90 + i * 9;
-                        for (int k = 0; k < 9; ++k) s_best[k] = Em[k];
+                        S.best_h = h0c + h;
+                        S.best_i = i;
                         maxgood = good;
                         niters = ransac_update_num_iters(g.prob, (double)(m - good) / m, 5, niters);
                     }
                 }
             }
-            s_niters = niters;
-            s_maxgood = maxgood;
-            s_iter = it;
+            S.iter = it;
+            S.niters = niters;
+            S.maxgood = maxgood;
+            *Sp = S;
         }
-        __syncthreads();
     }
-    if (tid == 0) {
-        const int maxgood = s_maxgood;
+}
+
+// E, info and the optional inlier mask of each pair.
+__global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
+    const int p = blockIdx.x;
+    const RansacState S = g.rs[p];
+    int32_t* info = g.info + (int64_t)p * 4;
+    double* E_out = g.E + (int64_t)p * 90;
+    const int m = S.m;
+    const int64_t base = (int64_t)p * g.hyp_cap;
+    if (m < 5) {
+        if (threadIdx.x == 0) {
+            info[0] = info[1] = info[2] = 0;
+            info[3] = DVO_EFEWPTS;
+        }
+        return;
+    }
+    if (m == 5) {
+        const int k = g.nmod[base];
+        if (threadIdx.x == 0) {
+            info[0] = 3 * k;
+            info[1] = k > 0 ? 5 : 0;
+            info[2] = 1;
+            info[3] = k > 0 ? DVO_OK : DVO_ENOMODEL;
+        }
+        for (int e = threadIdx.x; e < k * 9; e += 256) E_out[e] = g.models[base * 90 + e];
+        if (g.mask && k > 0 && threadIdx.x < 5) g.mask[(int64_t)p * g.pts_stride + threadIdx.x] = 1;
+        return;
+    }
+    const int maxgood = S.maxgood;
+    if (threadIdx.x == 0) {
         info[0] = maxgood > 0 ? 3 : 0;
         info[1] = maxgood;
-        info[2] = s_iter;
+        info[2] = S.iter;
         info[3] = maxgood > 0 ? DVO_OK : DVO_ENOMODEL;
-        if (maxgood > 0)
-            for (int k = 0; k < 9; ++k) E_out[k] = s_best[k];
     }
+    if (maxgood <= 0) return;
+    const double* Eb = g.models + (base + S.best_h) * 90 + S.best_i * 9;
+    if (threadIdx.x < 9) E_out[threadIdx.x] = Eb[threadIdx.x];
     if (g.mask) {
-        __syncthreads();
-        if (s_maxgood > 0)
-            for (int j = tid; j < m; j += kRNT) {
-                const double* pt = npts + (int64_t)j * 4;
-                g.mask[(int64_t)p * g.pts_stride + j] = sampson_err(s_best, pt[0], pt[1], pt[2], pt[3]) <= t;
-            }
+        double Ed[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Ed[k] = Eb[k];
+        const double thr = g.threshold / ((g.fx + g.fy) / 2);
+        const float t = (float)(thr * thr);
+        const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
+        for (int j = threadIdx.x; j < m; j += 256) {
+            const double* pt = npts + (int64_t)j * 4;
+            g.mask[(int64_t)p * g.pts_stride + j] = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]) <= t;
+        }
     }
+}
+
+hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
+    const int cap = g.hyp_cap;
+    for (int round = 0; round < 2; ++round) {
+        const int span = round == 0 ? min(kRansacRound1, cap) : cap - kRansacRound1;
+        if (span <= 0) break;
+        hipLaunchKernelGGL(ransac_sample_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs, round);
+        const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
+        hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
+        hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
+        hipLaunchKernelGGL(ransac_dk_kernel, dim3(kDkBlocks), dim3(kDkNT), 0, s, g, pairs);
+        hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
+        hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
+                           s, g);
+        hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
+    }
+    hipLaunchKernelGGL(ransac_finish_kernel, dim3(pairs), dim3(256), 0, s, g);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -1161,17 +1645,24 @@ __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, 
     if (i < n) out[i] = ransac_update_num_iters(p, ep[i], mp, mi);
 }
 
-__global__ void test_five_point_kernel(const double* qin, double* models, int* n) {
+__device__ double g_test_gscr[200 * 64];
+__device__ double g_test_rec[kRecDoubles * 64];
+__global__ __launch_bounds__(64) void test_five_point_kernel(const double* qin, double* models, int* n) {
+    __shared__ double lds_g[36 * 64];
+    if (threadIdx.x != 0) return;
     double q[5][4];
     for (int i = 0; i < 5; ++i)
         for (int k = 0; k < 4; ++k) q[i][k] = qin[i * 4 + k];
-    *n = five_point(q, models);
+    *n = five_point(q, models, lds_g, g_test_gscr, g_test_rec);
 }
 
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s) {
     if (pairs <= 0) return hipSuccess;
     if (stages & kStageNormalize) hipLaunchKernelGGL(normalize_kernel, dim3(4, pairs), dim3(256), 0, s, g);
-    if (stages & kStageRansac) hipLaunchKernelGGL(ransac_kernel, dim3(pairs), dim3(kRNT), 0, s, g);
+    if (stages & kStageRansac) {
+        hipError_t e = launch_ransac(g, pairs, s);
+        if (e != hipSuccess) return e;
+    }
     if (stages & kStagePose) hipLaunchKernelGGL(recover_pose_kernel, dim3(pairs), dim3(kPNT), 0, s, g);
     return hipGetLastError();
 }
@@ -1227,8 +1718,20 @@ hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int
 }
 
 hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n, hipStream_t s) {
-    hipLaunchKernelGGL(test_five_point_kernel, dim3(1), dim3(1), 0, s, d_q, d_models, d_n);
+    hipLaunchKernelGGL(test_five_point_kernel, dim3(1), dim3(64), 0, s, d_q, d_models, d_n);
     return hipGetLastError();
 }
 
 }  // namespace dvo
+
+#ifdef DVO_PROBE
+extern "C" int dvo_debug_probe(unsigned long long* out, int n, int reset) {
+    if (n > 32) n = 32;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dvo::g_probe), n * sizeof(unsigned long long)) != hipSuccess) return -4;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(dvo::g_probe), z, sizeof(z)) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#endif
