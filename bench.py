@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--pool", type=int, default=0, help="distinct frames rendered per rank (default 2*batch+1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP-event timing")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight: each on its own dvo_stream / HIP stream, so one batch's "
+                         "serial RANSAC tail overlaps the next batch's ORB")
     return ap.parse_args()
 
 
@@ -96,39 +99,52 @@ def main():
     torch.cuda.synchronize()
 
     ctx = Context(local_rank)
-    fs = FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
-    rec = fs.new_records(B)
+    S = max(1, args.streams)
+    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
+           for _ in range(S)]
+    for f in fss[1:]:
+        f.share_pose(fss[0])  # one pose stream across the alternating batches
+    recs_t = [f.new_records(B) for f in fss]
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     corners = torch.tensor(np.stack([scene.marker_corners(base + i) for i in range(pool_n)]), dtype=torch.float64,
                            device=dev)
-    T_rel = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
-    T_abs = torch.empty((B, 4, 4), dtype=torch.float64, device=dev)
-    fs.reset_pose()
-    gathered = torch.empty(world * rec.numel(), dtype=torch.uint8, device=dev) if world > 1 else None
+    T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    fss[0].reset_pose()
+    torch.cuda.synchronize()
+    gathered = [torch.empty(world * recs_t[0].numel(), dtype=torch.uint8, device=dev) for _ in range(S)] \
+        if world > 1 else None
     n_windows = max(1, (pool_n - 1) // B)
 
     def step(i):
         s = (i % n_windows) * B
-        fs.process(pool[s:s + B + 1], rec)
-        fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel, T_abs)
+        k = i % S
+        fs = fss[k]
+        fs.process(pool[s:s + B + 1], recs_t[k], wait_torch=False)
+        fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
         if world > 1:
-            fs.sync()  # records complete on the library's stream before RCCL reads them
-            dist.all_gather_into_tensor(gathered, rec)
+            # RCCL (on torch's stream) reads the records once the library's stream has written them
+            torch.cuda.current_stream().wait_event(fs.record_event())
+            dist.all_gather_into_tensor(gathered[k], recs_t[k])
+
+    def sync_all():
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
 
     for i in range(args.warmup):
         step(i)
-    fs.sync()
-    torch.cuda.synchronize()
+    sync_all()
     if not args.no_profile:
-        fs.set_profiling(True)
+        for f in fss:
+            f.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    fs.sync()
-    torch.cuda.synchronize()
+    sync_all()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -137,8 +153,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    recs = FrameStream.records_numpy(rec, B)
-    stage_ms, calls = (fs.stage_times() if not args.no_profile else ({}, 0))
+    recs = FrameStream.records_numpy(recs_t[(args.warmup + args.steps - 1) % S], B)
+    stage_ms, calls = {}, 0
+    if not args.no_profile:
+        for f in fss:
+            sm, c = f.stage_times()
+            calls += c
+            for kk, v in sm.items():
+                stage_ms[kk] = stage_ms.get(kk, 0.0) + v
     frames_total = B * args.steps * world
     value = frames_total / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -186,6 +208,7 @@ def main():
         "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, batch {B} new frames/step per GPU",
                    "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
                    "parallelism": f"frame-sharded x{world}" + (" + RCCL all_gather" if world > 1 else ""),
+                   "streams_in_flight": S,
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},
         "roofline": roofline,

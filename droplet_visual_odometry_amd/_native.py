@@ -90,6 +90,7 @@ _SIGNATURES = {
     "dvo_stream_hip_stream": ([_vp], _vp),
     "dvo_stream_set_profiling": ([_vp, _c], _c),
     "dvo_stream_reset_pose": ([_vp, _vp, _vp], _c),
+    "dvo_stream_share_pose": ([_vp, _vp], _c),
     "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),
     "dvo_stream_get_features": ([_vp, _c, _vp, _vp, _c, _ip], _c),

@@ -33,6 +33,10 @@ struct dvo_stream {
     std::vector<void*> allocs;
     uint8_t* d_frames = nullptr;  // per-call upload slab (max_frames images)
     double* d_carry = nullptr;    // pose tail carry: P_prev (12) | T_abs_prev (16)
+    hipEvent_t carry_ev = nullptr;  // recorded after every pose tail on this carry
+    bool carry_ev_valid = false;
+    dvo_stream* carry_owner = nullptr;  // stream whose carry this one uses (itself by default)
+    bool own_hs = false;
     int last_nframes = 0;
     bool last_has_pairs = false;  // the last call ran match + geometry
     hipStream_t hs = nullptr;
@@ -86,7 +90,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     int nper[kMaxLevels];
     features_per_level(nfeatures, kMaxLevels, nper);
     int64_t pyr = 0, blur = 0, bcand = 0, cand = 0;
-    int bands = 0, tiles = 0;
+    int bands = 0, tiles = 0, coef = 0;
     for (int l = 0; l < kMaxLevels; ++l) {
         LevelGeom& G = p.L[l];
         G.scale = (float)std::pow((double)1.2f, (double)l);  // getScale
@@ -94,10 +98,15 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         G.w = l == 0 ? w : cv_round_f(w * inv);
         G.h = l == 0 ? h : cv_round_f(h * inv);
         G.nper = nper[l];
+        G.pitch = (G.w + 15) & ~15;
+        G.bpitch = G.pitch;
         G.pyr_off = l == 0 ? 0 : pyr;
-        if (l > 0) pyr += (int64_t)G.w * G.h;
+        if (l > 0) pyr += (int64_t)G.pitch * G.h;
         G.blur_off = blur;
-        blur += (int64_t)G.w * G.h;
+        blur += (int64_t)G.bpitch * G.h;
+        G.xcoef_off = l == 0 ? 0 : coef;
+        G.ycoef_off = l == 0 ? 0 : coef + G.w;
+        if (l > 0) coef += G.w + G.h;
         const bool usable = G.w > 2 * kBorder && G.h > 2 * kBorder;
         const int rows = usable ? G.h - 2 * kBorder : 0;
         const int wc = usable ? G.w - 2 * kBorder : 0;
@@ -110,8 +119,8 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         G.cand_cap = G.nbands * G.band_cap + 4;
         G.cand_off = cand;
         cand += G.cand_cap;
-        G.tiles_x = (G.w + 63) / 64;
-        G.tiles_y = (G.h + 15) / 16;
+        G.tiles_x = (G.w + kBlurTW - 1) / kBlurTW;
+        G.tiles_y = (G.h + kBlurTH - 1) / kBlurTH;
         G.tile_base = tiles;
         tiles += G.tiles_x * G.tiles_y;
     }
@@ -121,8 +130,37 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     p.band_cand_stride = (bcand + 63) & ~(int64_t)63;
     p.cand_stride = (cand + 63) & ~(int64_t)63;
     p.total_tiles = tiles;
+    p.coef_total = coef;
     p.kp_cap = ((nfeatures + 256) + 63) & ~63;
     return p;
+}
+
+// resize.cpp INTER_LINEAR_EXACT coefficient of destination index `val` (double
+// arithmetic as OpenCV's softdouble path; host and device agree bit for bit
+// because both are IEEE double without contraction).
+int lin_coef_packed(int val, int srcsize, int dstsize) {
+    const double inv_scale = (double)dstsize / srcsize;
+    const double scale = 1.0 / inv_scale;
+    const double fval = scale * ((double)val + 0.5) - 0.5;
+    const int ival = (int)std::floor(fval);
+    if (ival >= 0 && srcsize > 1) {
+        if (ival < srcsize - 1) {
+            const int c1 = (int)std::nearbyint((fval - (double)ival) * 256.0);
+            return ival | (c1 << 13);
+        }
+        return (srcsize - 1) | (2 << 22);
+    }
+    return 1 << 22;
+}
+
+std::vector<int32_t> resize_coefs(const Plan& p) {
+    std::vector<int32_t> c(std::max(p.coef_total, 1));
+    for (int l = 1; l < p.nlevels; ++l) {
+        const LevelGeom &S = p.L[l - 1], &D = p.L[l];
+        for (int x = 0; x < D.w; ++x) c[D.xcoef_off + x] = lin_coef_packed(x, S.w, D.w);
+        for (int y = 0; y < D.h; ++y) c[D.ycoef_off + y] = lin_coef_packed(y, S.h, D.h);
+    }
+    return c;
 }
 
 int check_orb_params(dvo_ctx* ctx, const dvo_orb_params* o) {
@@ -206,6 +244,9 @@ GeomArgs stream_geom(dvo_stream* s) {
     return g;
 }
 
+// Row pitch of the internal frame slab (word-aligned rows for the byte kernels).
+int frame_pitch(const dvo_stream* s) { return (s->cfg.width + 15) & ~15; }
+
 int stream_alloc(dvo_stream* s) {
     const int F = s->cfg.max_frames;
     const Plan& p = s->plan;
@@ -217,6 +258,7 @@ int stream_alloc(dvo_stream* s) {
         return rc;
     A(b.pyr, (size_t)F * p.pyr_stride);
     A(b.blur, (size_t)F * p.blur_stride);
+    A(b.coef, (size_t)std::max(p.coef_total, 1));
     A(b.band_cnt, (size_t)F * (p.total_bands + 1));
     A(b.band_cand, (size_t)F * p.band_cand_stride);
     A(b.cand, (size_t)F * p.cand_stride);
@@ -249,7 +291,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.info, (size_t)F * 4);
     A(b.Rt, (size_t)F * 12);
     A(b.good, (size_t)F);
-    A(s->d_frames, (size_t)F * s->cfg.width * s->cfg.height);
+    A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
     A(s->d_carry, (size_t)28);
 #undef A
     return DVO_OK;
@@ -372,10 +414,24 @@ int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** o
     s->cfg = *cfg;
     s->plan = make_plan(cfg->width, cfg->height, cfg->orb.nfeatures, cfg->orb.fast_threshold);
     if (s->plan.kp_cap > 65535) return fail(ctx, DVO_EINVAL, "too many features");
-    s->hs = ctx->stream;
+    if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess)
+        return fail(ctx, DVO_EHIP, "hipStreamCreate failed");
+    s->own_hs = true;
+    s->carry_owner = s.get();
+    if (hipEventCreateWithFlags(&s->carry_ev, hipEventDisableTiming) != hipSuccess) {
+        hipStreamDestroy(s->hs);
+        return fail(ctx, DVO_EHIP, "hipEventCreate failed");
+    }
     rc = stream_alloc(s.get());
+    if (!rc) {
+        const std::vector<int32_t> coefs = resize_coefs(s->plan);
+        if (hipMemcpy(s->buf.coef, coefs.data(), coefs.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(ctx, DVO_EHIP, "coefficient upload failed");
+    }
     if (rc) {
         for (void* p : s->allocs) hipFree(p);
+        hipEventDestroy(s->carry_ev);
+        hipStreamDestroy(s->hs);
         return rc;
     }
     *out = s.release();
@@ -390,17 +446,29 @@ void dvo_stream_destroy(dvo_stream* s) {
     for (auto* pool : {&s->ev_pending, &s->ev_free})
         for (auto& e : *pool)
             for (auto x : e) hipEventDestroy(x);
+    hipEventDestroy(s->carry_ev);
+    if (s->own_hs) hipStreamDestroy(s->hs);
     delete s;
 }
 
 int dvo_stream_reset_pose(dvo_stream* s, const double* P0, const double* T0) {
     if (!s || !P0 || !T0) return DVO_EINVAL;
     dvo_ctx* ctx = s->ctx;
+    dvo_stream* o = s->carry_owner;
     double c[28];
     std::memcpy(c, P0, 12 * sizeof(double));
     std::memcpy(c + 12, T0, 16 * sizeof(double));
-    HIP_TRY(hipMemcpyAsync(s->d_carry, c, sizeof(c), hipMemcpyHostToDevice, s->hs));
+    if (o->carry_ev_valid) HIP_TRY(hipStreamWaitEvent(s->hs, o->carry_ev, 0));
+    HIP_TRY(hipMemcpyAsync(o->d_carry, c, sizeof(c), hipMemcpyHostToDevice, s->hs));
+    HIP_TRY(hipEventRecord(o->carry_ev, s->hs));
+    o->carry_ev_valid = true;
     HIP_TRY(hipStreamSynchronize(s->hs));
+    return DVO_OK;
+}
+
+int dvo_stream_share_pose(dvo_stream* s, dvo_stream* owner) {
+    if (!s || !owner || owner->carry_owner != owner) return DVO_EINVAL;
+    s->carry_owner = owner;
     return DVO_OK;
 }
 
@@ -414,10 +482,14 @@ int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const doub
     const int pairs = s->last_nframes - 1;
     HIP_TRY(hipSetDevice(ctx->device));
     hipEvent_t* ev = (s->profiling && !s->ev_pending.empty()) ? s->ev_pending.back().data() : nullptr;
+    dvo_stream* o = s->carry_owner;  // pose tails on one carry run in call order, across streams
+    if (o->carry_ev_valid) HIP_TRY(hipStreamWaitEvent(s->hs, o->carry_ev, 0));
     mark(ev, 8, 0, s->hs);
     HIP_TRY(launch_pose_tail(s->buf.Rt, s->buf.info, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
-                             s->d_carry, d_T_rel, d_T_abs, s->hs));
+                             o->d_carry, d_T_rel, d_T_abs, s->hs));
     mark(ev, 8, 1, s->hs);
+    HIP_TRY(hipEventRecord(o->carry_ev, s->hs));
+    o->carry_ev_valid = true;
     return DVO_OK;
 }
 
@@ -450,6 +522,14 @@ int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int
     if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
     if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
     HIP_TRY(hipSetDevice(ctx->device));
+    if (((uintptr_t)d_frames | (uintptr_t)frame_stride | (uintptr_t)stride) & 3) {
+        // the byte kernels read level 0 in 4-byte words: realign into the slab
+        const int pw = frame_pitch(s);
+        for (int i = 0; i < n_frames; ++i)
+            HIP_TRY(hipMemcpy2DAsync(s->d_frames + (size_t)i * pw * s->cfg.height, pw, d_frames + i * frame_stride,
+                                     stride, s->cfg.width, s->cfg.height, hipMemcpyDeviceToDevice, s->hs));
+        return run_stream(s, s->d_frames, n_frames, (int64_t)pw * s->cfg.height, pw, d_records, false);
+    }
     return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false);
 }
 
@@ -513,12 +593,12 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
     if (cap < G.w * G.h) return fail(ctx, DVO_ECAP, "capacity too small");
     HIP_TRY(hipStreamSynchronize(s->hs));
     if (blurred) {
-        HIP_TRY(hipMemcpy(out, s->buf.blur + (size_t)frame * s->plan.blur_stride + G.blur_off, (size_t)G.w * G.h,
-                          hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(out, G.w, s->buf.blur + (size_t)frame * s->plan.blur_stride + G.blur_off, G.bpitch, G.w,
+                            G.h, hipMemcpyDeviceToHost));
     } else {
         if (level == 0) return fail(ctx, DVO_EINVAL, "level 0 is the input frame");
-        HIP_TRY(hipMemcpy(out, s->buf.pyr + (size_t)frame * s->plan.pyr_stride + G.pyr_off, (size_t)G.w * G.h,
-                          hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy2D(out, G.w, s->buf.pyr + (size_t)frame * s->plan.pyr_stride + G.pyr_off, G.pitch, G.w,
+                            G.h, hipMemcpyDeviceToHost));
     }
     return DVO_OK;
 }
@@ -554,8 +634,9 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
         ctx->call_nf = params->nfeatures;
     }
     dvo_stream* s = ctx->call_stream;
-    HIP_TRY(hipMemcpy2DAsync(s->d_frames, w, img, stride, w, h, hipMemcpyHostToDevice, s->hs));
-    rc = run_stream(s, s->d_frames, 1, (int64_t)w * h, w, nullptr, true);
+    const int pw = frame_pitch(s);
+    HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+    rc = run_stream(s, s->d_frames, 1, (int64_t)pw * h, pw, nullptr, true);
     if (rc) return rc;
     return dvo_stream_get_features(s, 0, kps, desc, cap, n_out);
 }

@@ -15,17 +15,21 @@
 namespace dvo {
 
 constexpr int kMaxLevels = 8;
-constexpr int kBandRows = 8;        // FAST band height (rows of output per workgroup)
+constexpr int kBandRows = 16;       // FAST band height (rows of output per workgroup)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
+constexpr int kBlurTW = 256, kBlurTH = 32;  // blur tile (4 px x 8 rows per thread)
 
 // Per-level geometry of one ORB plan (identical for every frame of a stream).
 struct LevelGeom {
     int w, h;
     float scale;          // getScale(l) = (float)pow(double(1.2f), l)
     int nper;             // features per level
+    int pitch;            // row pitch of level l (l >= 1) in the pyramid slab, multiple of 16
+    int bpitch;           // row pitch of level l in the blurred slab, multiple of 16
     int64_t pyr_off;      // byte offset of level l (l >= 1) in a frame's pyramid slab
     int64_t blur_off;     // byte offset of level l in a frame's blurred slab
+    int xcoef_off, ycoef_off;  // resize coefficient tables of level l (l >= 1) in Buffers::coef
     int nbands;           // FAST bands over rows [31, h-31)
     int band_base;        // first band index of this level within a frame
     int band_cap;         // candidate capacity per band
@@ -45,7 +49,15 @@ struct Plan {
     int64_t band_cand_stride; // u32 per frame
     int64_t cand_stride;      // u32 per frame
     int total_tiles;          // blur tiles per frame
+    int coef_total;           // ints in the resize coefficient table
 };
+
+// Resize coefficient of one destination column/row (resize.cpp INTER_LINEAR_EXACT):
+// bits 0..12 source offset, 13..21 c1 (0..256, c0 = 256 - c1), 22..23 mode
+// (0 interior, 1 clamp to src[0], 2 clamp to src[last]).
+__host__ __device__ inline int coef_ofs(int c) { return c & 0x1FFF; }
+__host__ __device__ inline int coef_c1(int c) { return (c >> 13) & 0x1FF; }
+__host__ __device__ inline int coef_mode(int c) { return (c >> 22) & 3; }
 
 // Device buffers of one stream (all sized for max_frames).
 // Per-pair RANSAC state carried between the batch-wide round kernels
@@ -65,6 +77,7 @@ constexpr int kRansacRound1 = 256;  // hypotheses per pair in round 1
 struct Buffers {
     uint8_t* pyr;
     uint8_t* blur;
+    int32_t* coef;        // resize coefficient tables (Plan::coef_total ints)
     int32_t* band_cnt;
     uint32_t* band_cand;
     uint32_t* cand;       // gathered candidate keys (score<<24 | y<<12 | x)
@@ -111,7 +124,7 @@ struct StreamParams {   // passed by value to every batch kernel
 __host__ __device__ inline const uint8_t* level_ptr(const StreamParams& P, int f, int l) {
     return l == 0 ? P.frames + (int64_t)f * P.frame_stride : P.buf.pyr + (int64_t)f * P.plan.pyr_stride + P.plan.L[l].pyr_off;
 }
-__host__ __device__ inline int level_pitch(const StreamParams& P, int l) { return l == 0 ? P.in_pitch : P.plan.L[l].w; }
+__host__ __device__ inline int level_pitch(const StreamParams& P, int l) { return l == 0 ? P.in_pitch : P.plan.L[l].pitch; }
 __host__ __device__ inline uint8_t* blur_ptr(const StreamParams& P, int f, int l) {
     return P.buf.blur + (int64_t)f * P.plan.blur_stride + P.plan.L[l].blur_off;
 }

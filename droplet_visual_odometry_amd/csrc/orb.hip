@@ -35,113 +35,143 @@ constexpr int kCdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1}
 constexpr int kCdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
 // ------------------------------------------------------------------------
-// Level l from level l-1: resize.cpp resize_bitExact<uchar, interpolationLinear>.
-struct LinCoef {
-    int ofs, c0, c1, mode;  // mode 0 interior, 1 left edge (src[0]), 2 right edge (src[last])
-};
-
-__device__ LinCoef lin_coef(int val, int srcsize, int dstsize) {
-    const double inv_scale = (double)dstsize / srcsize;
-    const double scale = 1.0 / inv_scale;
-    double fval = scale * ((double)val + 0.5) - 0.5;
-    int ival = cv_floor_d(fval);
-    LinCoef c{0, 0, 0, 0};
-    if (ival >= 0 && srcsize > 1) {
-        if (ival < srcsize - 1) {
-            c.ofs = ival;
-            c.c1 = cv_round_d((fval - (double)ival) * 256.0);
-            c.c0 = 256 > c.c1 ? 256 - c.c1 : 0;
-        } else {
-            c.ofs = srcsize - 1;
-            c.mode = 2;
-        }
-    } else {
-        c.mode = 1;
-    }
-    return c;
-}
-
-// OpenCV decides edges from the running min/max over all positions; since
-// fval is monotone in val, "left edge" = prefix with ival < 0 and "right edge"
-// = suffix with ival >= srcsize-1, which is what lin_coef's mode encodes.
-__device__ __forceinline__ uint32_t hline(const uint8_t* row, const LinCoef& cx, int sw) {
-    if (cx.mode == 1) return (uint32_t)row[0] << 8;
-    if (cx.mode == 2) return (uint32_t)row[sw - 1] << 8;
-    return (uint32_t)cx.c0 * row[cx.ofs] + (uint32_t)cx.c1 * row[cx.ofs + 1];
+// Level l from level l-1: resize.cpp resize_bitExact<uchar, interpolationLinear>
+// (INTER_LINEAR_EXACT, 8-bit fixed point).  The per-column / per-row
+// coefficients are computed once per plan on the host (api.cpp resize_coefs,
+// same double arithmetic) and read from a table; each thread produces 4
+// adjacent output pixels of one row and stores them as one 32-bit word.
+__device__ __forceinline__ uint32_t hline_c(const uint8_t* row, int c, int sw) {
+    const int mode = coef_mode(c);
+    if (mode == 1) return (uint32_t)row[0] << 8;
+    if (mode == 2) return (uint32_t)row[sw - 1] << 8;
+    const int ofs = coef_ofs(c), c1 = coef_c1(c);
+    return (uint32_t)(256 - c1) * row[ofs] + (uint32_t)c1 * row[ofs + 1];
 }
 
 __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l) {
     const int f = blockIdx.z;
     const LevelGeom& S = P.plan.L[l - 1];
     const LevelGeom& D = P.plan.L[l];
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
     const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx >= D.w || dy >= D.h) return;
+    if (x0 >= D.w || dy >= D.h) return;
     const uint8_t* src = level_ptr(P, f, l - 1);
     const int sp = level_pitch(P, l - 1);
-    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
-    LinCoef cx = lin_coef(dx, S.w, D.w);
-    LinCoef cy = lin_coef(dy, S.h, D.h);
-    uint32_t v;
-    if (cy.mode != 0) {
-        const uint8_t* row = src + (int64_t)(cy.mode == 1 ? 0 : S.h - 1) * sp;
-        uint32_t hh = hline(row, cx, S.w);
-        v = (hh + 128) >> 8;
-    } else {
-        uint32_t h0 = hline(src + (int64_t)cy.ofs * sp, cx, S.w);
-        uint32_t h1 = hline(src + (int64_t)(cy.ofs + 1) * sp, cx, S.w);
-        v = (h0 * (uint32_t)cy.c0 + h1 * (uint32_t)cy.c1 + 32768u) >> 16;
+    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off + (int64_t)dy * D.pitch;
+    const int cy = P.buf.coef[D.ycoef_off + dy];
+    const int ymode = coef_mode(cy);
+    const uint8_t* r0 = src + (int64_t)(ymode == 0 ? coef_ofs(cy) : (ymode == 1 ? 0 : S.h - 1)) * sp;
+    const uint8_t* r1 = r0 + sp;
+    const uint32_t cy1 = coef_c1(cy), cy0 = 256 - cy1;
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int dx = x0 + j;
+        if (dx < D.w) {
+            const int cx = P.buf.coef[D.xcoef_off + dx];
+            uint32_t v;
+            if (ymode != 0) {
+                v = (hline_c(r0, cx, S.w) + 128) >> 8;
+            } else {
+                v = (hline_c(r0, cx, S.w) * cy0 + hline_c(r1, cx, S.w) * cy1 + 32768u) >> 16;
+            }
+            word |= (v > 255 ? 255u : v) << (8 * j);
+        }
     }
-    dst[(int64_t)dy * D.w + dx] = (uint8_t)(v > 255 ? 255 : v);
+    if (x0 + 4 <= D.w) {
+        *reinterpret_cast<uint32_t*>(dst + x0) = word;
+    } else {
+        for (int j = 0; j < 4 && x0 + j < D.w; ++j) dst[x0 + j] = (uint8_t)(word >> (8 * j));
+    }
 }
 
 // ------------------------------------------------------------------------
 // GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) with the 8-bit kernel
-// {18,34,49,55,49,34,18}: int row sums, (colsum + 2^15) >> 16.
-constexpr int kBTX = 64, kBTY = 16;
+// {18,34,49,55,49,34,18}: int row sums, (colsum + 2^15) >> 16, saturated.
+// Each thread owns 4 adjacent columns and 8 output rows of a 256 x 32 tile:
+// it walks the 14 input rows once, forms the 4 horizontal 7-tap sums of a row
+// with two v_dot4_u32_u8 per pixel on byte-aligned windows (v_alignbyte of
+// three row words), keeps a rolling 7-row window in registers and emits 4
+// pixels per row as one word.  Border columns gather bytes through reflect-101.
 __device__ __forceinline__ int refl101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
     return p;
 }
 
+constexpr uint32_t kGk0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
+constexpr uint32_t kGk1 = 49u | (34u << 8) | (18u << 16);
+
 __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
     const int f = blockIdx.y;
-    int item = blockIdx.x;
+    const int item = blockIdx.x;
     int l = 0;
     while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].tile_base) ++l;
     const LevelGeom& G = P.plan.L[l];
     const int t = item - G.tile_base;
-    const int tx0 = (t % G.tiles_x) * kBTX, ty0 = (t / G.tiles_x) * kBTY;
+    const int ty = t / G.tiles_x, tx = t - ty * G.tiles_x;
+    const int x0 = tx * kBlurTW + 4 * (threadIdx.x & 63);
+    const int y0 = ty * kBlurTH + 8 * (threadIdx.x >> 6);
+    const int w = G.w, h = G.h;
+    if (x0 >= w || y0 >= h) return;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
     uint8_t* dst = blur_ptr(P, f, l);
-    __shared__ uint8_t tile[kBTY + 6][kBTX + 6];
-    __shared__ int rows[kBTY + 6][kBTX];
-    for (int i = threadIdx.x; i < (kBTY + 6) * (kBTX + 6); i += 256) {
-        int ry = i / (kBTX + 6), rx = i % (kBTX + 6);
-        int y = refl101(ty0 + ry - 3, G.h), x = refl101(tx0 + rx - 3, G.w);
-        tile[ry][rx] = src[(int64_t)y * sp + x];
-    }
-    __syncthreads();
-    const int k[7] = {18, 34, 49, 55, 49, 34, 18};
-    for (int i = threadIdx.x; i < (kBTY + 6) * kBTX; i += 256) {
-        int ry = i / kBTX, rx = i % kBTX;
-        int s = 0;
+    const bool interior = x0 >= 4 && x0 + 8 <= w;
+    uint32_t hs[7][4];
 #pragma unroll
-        for (int j = 0; j < 7; ++j) s += k[j] * tile[ry][rx + j];
-        rows[ry][rx] = s;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kBTY * kBTX; i += 256) {
-        int ry = i / kBTX, rx = i % kBTX;
-        int y = ty0 + ry, x = tx0 + rx;
-        if (y >= G.h || x >= G.w) continue;
-        int s = 0;
+    for (int r = 0; r < 14; ++r) {
+        const uint8_t* row = src + (int64_t)refl101(y0 - 3 + r, h) * sp;
+        uint32_t wm, w0, w1;
+        if (interior) {
+            wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
+            w0 = *reinterpret_cast<const uint32_t*>(row + x0);
+            w1 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
+        } else {
+            uint32_t b[3] = {0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 7; ++j) s += k[j] * rows[ry + j][rx];
-        int v = (s + (1 << 15)) >> 16;
-        dst[(int64_t)y * G.w + x] = (uint8_t)(v > 255 ? 255 : v);
+            for (int k = 0; k < 12; ++k) b[k >> 2] |= (uint32_t)row[refl101(x0 - 4 + k, w)] << (8 * (k & 3));
+            wm = b[0];
+            w0 = b[1];
+            w1 = b[2];
+        }
+        // taps of output x0+j: bytes x0+j-3 .. x0+j+3 = window offsets j+1 .. j+7 of (wm, w0, w1)
+        uint32_t hcur[4];
+        hcur[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 1), kGk0,
+                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), kGk1, 0u, false),
+                                         false);
+        hcur[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 2), kGk0,
+                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), kGk1, 0u, false),
+                                         false);
+        hcur[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 3), kGk0,
+                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), kGk1, 0u, false),
+                                         false);
+        hcur[3] = __builtin_amdgcn_udot4(w0, kGk0, __builtin_amdgcn_udot4(w1, kGk1, 0u, false), false);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) hs[k][j] = hs[k + 1][j];
+            hs[6][j] = hcur[j];
+        }
+        if (r >= 6) {
+            const int y = y0 + r - 6;
+            if (y < h) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t sum = 18u * hs[0][j] + 34u * hs[1][j] + 49u * hs[2][j] + 55u * hs[3][j] +
+                                         49u * hs[4][j] + 34u * hs[5][j] + 18u * hs[6][j];
+                    const uint32_t v = (sum + (1u << 15)) >> 16;
+                    word |= (v > 255 ? 255u : v) << (8 * j);
+                }
+                uint8_t* drow = dst + (int64_t)y * G.bpitch;
+                if (x0 + 4 <= w) {
+                    *reinterpret_cast<uint32_t*>(drow + x0) = word;
+                } else {
+                    for (int j = 0; j < 4 && x0 + j < w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+                }
+            }
+        }
     }
 }
 
@@ -216,6 +246,17 @@ __device__ __forceinline__ int block_excl_scan(int v, int& total, int* lds) {
     return off + x - v;
 }
 
+__device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  // byte k of (hi:lo), k in [0, 8)
+    return k < 4 ? (lo >> (8 * k)) & 0xFF : (hi >> (8 * (k - 4))) & 0xFF;
+}
+
+// One band of kBandRows output rows of one level: the band's image rows (+4
+// halo) are loaded into LDS as words; FAST scores are computed for rows
+// [r0-1, r1] (the NMS neighbourhood).  Every pixel first takes the compass
+// test (a run of 9 on the 16-circle covers >= 2 of the pixels 0, 4, 8, 12),
+// survivors are compacted per wave and only they run the full test + score.
+// Strict 3x3 NMS then emits keys in raster order: per-row counts, a prefix
+// over rows, and within a row ballot ranks in column order.
 __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int f = blockIdx.y;
     const int item = blockIdx.x;
@@ -231,74 +272,152 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int sp = level_pitch(P, l);
     const int SW = ((w + 3) & ~3) + 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* img = smem;                       // 16 rows: y in [r0-4, r0+12)
-    uint8_t* sc = smem + 16 * SW;              // 10 rows: y in [r0-1, r0+9)
-    __shared__ int scan_lds[16];
-    const int ylo = r0 - 4, yhi = min(r0 + 12, h);
-    // load rows (bytes; rows are short and L2-resident)
-    for (int i = threadIdx.x; i < (yhi - ylo) * w; i += kFastNT) {
-        int ry = i / w, x = i - ry * w;
-        img[ry * SW + x] = src[(int64_t)(ylo + ry) * sp + x];
+    uint8_t* img = smem;                                   // rows [r0-4, r0+kBandRows+4)
+    uint8_t* sc = smem + (kBandRows + 8) * SW;             // rows [r0-1, r0+kBandRows+1)
+    __shared__ uint16_t queue[kFastNT / 64][256];
+    __shared__ int row_cnt[kBandRows], row_off[kBandRows + 1];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int ylo = r0 - 4, yhi = min(r1 + 4, h);
+    const int nwords = (w + 3) >> 2;
+    for (int r = 0; r < yhi - ylo; ++r) {
+        const uint32_t* srow = reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp);
+        uint32_t* drow = reinterpret_cast<uint32_t*>(img + r * SW);
+        for (int i = threadIdx.x; i < nwords; i += kFastNT) drow[i] = srow[i];
     }
     __syncthreads();
-    // scores for rows [r0-1, r1] (NMS neighbourhood), columns in groups of 4
-    const int gx0 = 28, gx1 = ((w - 28) + 3) & ~3;   // [28, ~w-28)
-    const int ngx = (gx1 - gx0) / 4;
+    // ---- scores, rows [r0-1, r1], columns [28, w-30) in groups of 4
+    const unsigned long long lt = (1ull << lane) - 1;
     const int nsr = r1 - r0 + 2;
-    for (int i = threadIdx.x; i < nsr * ngx; i += kFastNT) {
-        int sr = i / ngx, g = i - sr * ngx;
-        int y = r0 - 1 + sr;
-        int x0 = gx0 + 4 * g;
-        const uint8_t* base = img + (y - ylo) * SW;
-        uint32_t out = 0;
+    for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
+        const int y = r0 - 1 + sr;
+        const uint8_t* row = img + (y - ylo) * SW;
+        uint8_t* srow = sc + sr * SW;
+        for (int xb = 28; xb < w - 30; xb += 256) {
+            const int x0 = xb + 4 * lane;
+            uint32_t cmask = 0;
+            if (x0 < w - 30) {
+                *reinterpret_cast<uint32_t*>(srow + x0) = 0;
+                const uint32_t up = *reinterpret_cast<const uint32_t*>(row - 3 * SW + x0);
+                const uint32_t dn = *reinterpret_cast<const uint32_t*>(row + 3 * SW + x0);
+                const uint32_t wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
+                const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0);
+                const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int x = x0 + j;
-            int score = 0;
-            if (x >= 3 && x <= w - 4 && y >= 3 && y <= h - 4) {
-                int v = base[x];
+                for (int j = 0; j < 4; ++j) {
+                    const int v = (w0 >> (8 * j)) & 0xFF;
+                    const int c0 = (dn >> (8 * j)) & 0xFF;        // k = 0: (0, +3)
+                    const int c4 = byte_at(w0, w1, j + 3);       // k = 4: (+3, 0)
+                    const int c8 = (up >> (8 * j)) & 0xFF;        // k = 8: (0, -3)
+                    const int c12 = byte_at(wm, w0, j + 1);      // k = 12: (-3, 0)
+                    const int hi = v + thr, lo = v - thr;
+                    const int nb = (c0 > hi) + (c4 > hi) + (c8 > hi) + (c12 > hi);
+                    const int nd = (c0 < lo) + (c4 < lo) + (c8 < lo) + (c12 < lo);
+                    const int x = x0 + j;
+                    if ((nb >= 2 || nd >= 2) && x >= 3 && x <= w - 4) cmask |= 1u << j;
+                }
+            }
+            int base = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned long long bal = __ballot((cmask >> j) & 1);
+                if ((cmask >> j) & 1) queue[wid][base + __popcll(bal & lt)] = (uint16_t)(x0 + j);
+                base += __popcll(bal);
+            }
+            for (int q = lane; q < base; q += 64) {
+                const int x = queue[wid][q];
+                const int v = row[x];
                 int c[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) c[k] = base[kCdy[k] * SW + x + kCdx[k]];
+                for (int k = 0; k < 16; ++k) c[k] = row[kCdy[k] * SW + x + kCdx[k]];
                 uint32_t br = 0, dk = 0;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
                     br |= (uint32_t)(c[k] > v + thr) << k;
                     dk |= (uint32_t)(c[k] < v - thr) << k;
                 }
-                if (has_run9(br) || has_run9(dk)) score = fast_score16(c, v, thr);
+                if (has_run9(br) || has_run9(dk)) srow[x] = (uint8_t)fast_score16(c, v, thr);
             }
-            out |= (uint32_t)(score & 0xFF) << (8 * j);
         }
-        *reinterpret_cast<uint32_t*>(sc + sr * SW + x0) = out;
     }
     __syncthreads();
-    // NMS + raster-ordered compaction over rows [r0, r1), cols [31, w-31)
-    const int Wc = w - 2 * kBorder;
-    const int total = (r1 - r0) * Wc;
-    const int chunk = (total + kFastNT - 1) / kFastNT;
-    const int p0 = threadIdx.x * chunk, p1 = min(p0 + chunk, total);
-    auto keep = [&](int p, int& score, int& x, int& y) {
-        y = r0 + p / Wc;
-        x = kBorder + p % Wc;
-        const uint8_t* s = sc + (y - (r0 - 1)) * SW + x;
-        score = s[0];
-        return score > 0 && score > s[-1] && score > s[1] && score > s[-SW - 1] && score > s[-SW] &&
-               score > s[-SW + 1] && score > s[SW - 1] && score > s[SW] && score > s[SW + 1];
+    // ---- strict 3x3 NMS over rows [r0, r1), columns [31, w-31), raster order
+    auto keep_mask = [&](int y, int x0, uint32_t (&score)[4]) {
+        const uint8_t* s0 = sc + (y - (r0 - 1)) * SW;
+        uint32_t m = 0;
+        if (x0 < w - 31) {
+            const uint32_t a[3][3] = {
+                {*reinterpret_cast<const uint32_t*>(s0 - SW + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 - SW + x0),
+                 *reinterpret_cast<const uint32_t*>(s0 - SW + x0 + 4)},
+                {*reinterpret_cast<const uint32_t*>(s0 + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 + x0),
+                 *reinterpret_cast<const uint32_t*>(s0 + x0 + 4)},
+                {*reinterpret_cast<const uint32_t*>(s0 + SW + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 + SW + x0),
+                 *reinterpret_cast<const uint32_t*>(s0 + SW + x0 + 4)}};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int x = x0 + j;
+                const uint32_t v = byte_at(a[1][1], a[1][2], j);
+                score[j] = v;
+                const uint32_t l0 = j == 0 ? byte_at(a[0][0], a[0][1], 3) : byte_at(a[0][1], a[0][2], j - 1);
+                const uint32_t l1 = j == 0 ? byte_at(a[1][0], a[1][1], 3) : byte_at(a[1][1], a[1][2], j - 1);
+                const uint32_t l2 = j == 0 ? byte_at(a[2][0], a[2][1], 3) : byte_at(a[2][1], a[2][2], j - 1);
+                const uint32_t m0 = byte_at(a[0][1], a[0][2], j), m2 = byte_at(a[2][1], a[2][2], j);
+                const uint32_t q0 = byte_at(a[0][1], a[0][2], j + 1), q1 = byte_at(a[1][1], a[1][2], j + 1),
+                               q2 = byte_at(a[2][1], a[2][2], j + 1);
+                const bool k = x >= kBorder && x < w - kBorder && v > 0 && v > l0 && v > l1 && v > l2 && v > m0 &&
+                               v > m2 && v > q0 && v > q1 && v > q2;
+                m |= (uint32_t)k << j;
+            }
+        }
+        return m;
     };
-    int cnt = 0;
-    for (int p = p0; p < p1; ++p) {
-        int s, x, y;
-        cnt += keep(p, s, x, y);
+    const int nrows = r1 - r0;
+    for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
+        int cnt = 0;
+        for (int xb = 28; xb < w - 31; xb += 256) {
+            uint32_t score[4];
+            cnt += __popc(keep_mask(r0 + rr, xb + 4 * lane, score));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if (lane == 0) row_cnt[rr] = cnt;
     }
-    int tot;
-    int off = block_excl_scan(cnt, tot, scan_lds);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int rr = 0; rr < nrows; ++rr) {
+            row_off[rr] = acc;
+            acc += row_cnt[rr];
+        }
+        row_off[nrows] = acc;
+        P.buf.band_cnt[(int64_t)f * P.plan.total_bands + item] = acc;
+    }
+    __syncthreads();
     uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)b * G.band_cap;
-    for (int p = p0; p < p1; ++p) {
-        int s, x, y;
-        if (keep(p, s, x, y)) outp[off++] = ((uint32_t)s << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+    for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
+        const int y = r0 + rr;
+        int base = row_off[rr];
+        for (int xb = 28; xb < w - 31; xb += 256) {
+            const int x0 = xb + 4 * lane;
+            uint32_t score[4];
+            const uint32_t m = keep_mask(y, x0, score);
+            unsigned long long bal[4];
+            int before = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bal[j] = __ballot((m >> j) & 1);
+                before += __popcll(bal[j] & lt);
+            }
+            int mine = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((m >> j) & 1) {
+                    outp[base + before + mine] = (score[j] << 24) | ((uint32_t)y << 12) | (uint32_t)(x0 + j);
+                    ++mine;
+                }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) base += __popcll(bal[j]);
+        }
     }
-    if (threadIdx.x == 0) P.buf.band_cnt[(int64_t)f * P.plan.total_bands + item] = tot;
 }
 
 // ------------------------------------------------------------------------
@@ -702,7 +821,7 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     const float ang = angle * (float)(M_PI / 180.f);
     const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
     const uint8_t* bl = blur_ptr(P, f, l);
-    const int bstep = G.w;
+    const int bstep = G.bpitch;
     const uint8_t* bc = bl + (int64_t)cv_round_f(pty * sc) * bstep + cv_round_f(ptx * sc);
     unsigned long long words[4];
 #pragma unroll
@@ -748,7 +867,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const int F = P.nframes;
     mark(ev, 0, 0, s);
     for (int l = 1; l < pl.nlevels; ++l) {
-        dim3 grid((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F);
+        dim3 grid((pl.L[l].w + 255) / 256, (pl.L[l].h + 3) / 4, F);
         hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
     }
     mark(ev, 0, 1, s);
@@ -756,7 +875,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles, F), dim3(256), 0, s, P);
     mark(ev, 1, 1, s);
     const int SW = ((pl.L[0].w + 3) & ~3) + 16;
-    const size_t fast_lds = (size_t)(16 + 10) * SW;
+    const size_t fast_lds = (size_t)(2 * kBandRows + 10) * SW;
     mark(ev, 2, 0, s);
     if (pl.total_bands > 0)
         hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), fast_lds, s, P);

@@ -34,6 +34,7 @@ class FrameStream:
         h = _vp()
         self.ctx.check(self.ctx.lib.dvo_stream_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
+        self._ext = torch.cuda.ExternalStream(self.hip_stream, device=self.device)
         self.width, self.height, self.max_frames, self.nfeatures = width, height, max_frames, nfeatures
         self.K = K.reshape(3, 3)
 
@@ -44,8 +45,10 @@ class FrameStream:
     def new_records(self, n_pairs: int) -> torch.Tensor:
         return torch.zeros(max(n_pairs, 1) * PAIR_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
 
-    def process(self, frames: torch.Tensor, records: torch.Tensor | None = None) -> torch.Tensor:
-        """Enqueue the batch on the stream's HIP stream (asynchronous)."""
+    def process(self, frames: torch.Tensor, records: torch.Tensor | None = None, wait_torch: bool = True) -> torch.Tensor:
+        """Enqueue the batch on the stream's HIP stream (asynchronous).  With
+        wait_torch the batch is ordered after work queued on torch's current
+        stream (the frames' producer); pass False for frames already resident."""
         if frames.dtype != torch.uint8 or frames.dim() != 3 or not frames.is_cuda:
             raise ValueError("frames must be a uint8 [n, H, W] device tensor")
         n, h, w = frames.shape
@@ -55,9 +58,29 @@ class FrameStream:
             raise ValueError("frames rows must be contiguous")
         if records is None:
             records = self.new_records(n - 1)
+        if wait_torch:
+            self._after_torch()
         self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
                                                        frames.stride(1), records.data_ptr() if n > 1 else None))
         return records
+
+    def _after_torch(self):
+        """Order the library's HIP stream after work already queued on torch's
+        current stream (frames / corners produced by torch)."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._ext.wait_event(ev)
+
+    def record_event(self) -> torch.cuda.Event:
+        """An event on the library's stream after everything enqueued so far."""
+        ev = torch.cuda.Event()
+        ev.record(self._ext)
+        return ev
+
+    def share_pose(self, owner: "FrameStream"):
+        """Chain this stream's pose tails on `owner`'s carry (batches alternating
+        between streams form one pose stream)."""
+        self.ctx.check(self.ctx.lib.dvo_stream_share_pose(self.h, owner.h))
 
     def reset_pose(self, P0=None, T0=None):
         """Carry-in of the pose tail: P_prev (3x4, default K[I|0] as in controlled
@@ -68,7 +91,7 @@ class FrameStream:
                                                           ptr(np.ascontiguousarray(T0))))
 
     def pose_tail(self, corners_prev: torch.Tensor, corners_cur: torch.Tensor, marker_length: float,
-                  T_rel: torch.Tensor | None = None, T_abs: torch.Tensor | None = None):
+                  T_rel: torch.Tensor | None = None, T_abs: torch.Tensor | None = None, wait_torch: bool = True):
         """Device pose tail for the last processed batch (see dvo.h); corners are
         float64 [pairs, k, 2] device tensors.  Returns (T_rel, T_abs) [pairs, 4, 4]."""
         pairs, k = corners_prev.shape[0], corners_prev.shape[1]
@@ -76,6 +99,8 @@ class FrameStream:
             T_rel = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
         if T_abs is None:
             T_abs = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
+        if wait_torch:
+            self._after_torch()
         self.ctx.check(self.ctx.lib.dvo_stream_pose_tail(self.h, corners_prev.data_ptr(), corners_cur.data_ptr(), k,
                                                          float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
         return T_rel, T_abs

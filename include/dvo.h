@@ -129,7 +129,8 @@ void dvo_stream_destroy(dvo_stream* s);
 int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
                        dvo_pair_record* d_records);
 int dvo_stream_sync(dvo_stream* s);
-/* HIP stream the batch runs on (hipStream_t as void*), for event timing. */
+/* HIP stream the batch runs on (hipStream_t as void*; each dvo_stream owns
+ * one, so batches on different dvo_streams may overlap on the device). */
 void* dvo_stream_hip_stream(dvo_stream* s);
 /* Pose tail of get_transformation_between_two_frames (v3:309-345) and
  * previous_current_matching (v3:367) for the pairs of the last
@@ -142,6 +143,10 @@ void* dvo_stream_hip_stream(dvo_stream* s);
  * dvo_stream_reset_pose (controlled mode: P0 = K [I | 0], v3:164-166).
  * d_corners_*: device [pairs][k][2] doubles (k >= 2).  Outputs device [pairs][16]. */
 int dvo_stream_reset_pose(dvo_stream* s, const double* P0 /* host 12 */, const double* T0 /* host 16 */);
+/* Make s use owner's pose carry, so batches alternating between streams (each
+ * stream runs on its own HIP stream; batches overlap on the device) chain one
+ * pose stream: pose tails on a shared carry run in call order via HIP events. */
+int dvo_stream_share_pose(dvo_stream* s, dvo_stream* owner);
 int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
                          double marker_length, double* d_T_rel, double* d_T_abs);
 

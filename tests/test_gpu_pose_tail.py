@@ -50,3 +50,36 @@ def test_pose_tail_requires_process(gpu_ctx):
     with pytest.raises(DVOError):
         fs.pose_tail(c, c, 0.1)
     fs.close()
+
+
+def test_two_streams_share_one_pose_chain(gpu_ctx):
+    """Batches alternating between two dvo_streams (own HIP streams, overlapping
+    on the device) with a shared carry give the single-stream pose chain."""
+    import torch
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    frames, K = synth_frames(640, 480, range(7))
+    dev = torch.from_numpy(frames).cuda()
+    dc = torch.from_numpy(np.stack([marker_corners(i, K) for i in range(7)])).cuda()
+    ref = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    ref.reset_pose()
+    want = []
+    for start in (0, 3):
+        ref.process(dev[start:start + 4])
+        want.append(ref.pose_tail(dc[start:start + 3], dc[start + 1:start + 4], MARKER_LEN)[1])
+    ref.sync()
+    a = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    b = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    b.share_pose(a)
+    a.reset_pose()
+    got = []
+    for fs, start in ((a, 0), (b, 3)):
+        fs.process(dev[start:start + 4])
+        got.append(fs.pose_tail(dc[start:start + 3], dc[start + 1:start + 4], MARKER_LEN)[1])
+    a.sync()
+    b.sync()
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g.cpu().numpy(), w.cpu().numpy())
+    for fs in (ref, a, b):
+        fs.close()
