@@ -118,10 +118,12 @@ __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
     const int sp = level_pitch(P, l);
     uint8_t* dst = blur_ptr(P, f, l);
     const bool interior = x0 >= 4 && x0 + 8 <= w;
+    const bool rows_inside = y0 >= 3 && y0 + 10 < h;
     uint32_t hs[7][4];
 #pragma unroll
     for (int r = 0; r < 14; ++r) {
-        const uint8_t* row = src + (int64_t)refl101(y0 - 3 + r, h) * sp;
+        const int yy = y0 - 3 + r;
+        const uint8_t* row = src + (int64_t)(rows_inside ? yy : refl101(yy, h)) * sp;
         uint32_t wm, w0, w1;
         if (interior) {
             wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
@@ -159,8 +161,11 @@ __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
                 uint32_t word = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t sum = 18u * hs[0][j] + 34u * hs[1][j] + 49u * hs[2][j] + 55u * hs[3][j] +
-                                         49u * hs[4][j] + 34u * hs[5][j] + 18u * hs[6][j];
+                    // row sums < 2^16, weights < 2^8: 24-bit multiplies are exact
+                    const uint32_t sum = __umul24(18u, hs[0][j]) + __umul24(34u, hs[1][j]) +
+                                         __umul24(49u, hs[2][j]) + __umul24(55u, hs[3][j]) +
+                                         __umul24(49u, hs[4][j]) + __umul24(34u, hs[5][j]) +
+                                         __umul24(18u, hs[6][j]);
                     const uint32_t v = (sum + (1u << 15)) >> 16;
                     word |= (v > 255 ? 255u : v) << (8 * j);
                 }
@@ -274,7 +279,8 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* img = smem;                                   // rows [r0-4, r0+kBandRows+4)
     uint8_t* sc = smem + (kBandRows + 8) * SW;             // rows [r0-1, r0+kBandRows+1)
-    __shared__ uint16_t queue[kFastNT / 64][256];
+    constexpr int kRing = 512;                             // per-wave candidate ring (power of 2)
+    __shared__ uint32_t ring[kFastNT / 64][kRing];
     __shared__ int row_cnt[kBandRows], row_off[kBandRows + 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
@@ -285,9 +291,34 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
         for (int i = threadIdx.x; i < nwords; i += kFastNT) drow[i] = srow[i];
     }
     __syncthreads();
-    // ---- scores, rows [r0-1, r1], columns [28, w-30) in groups of 4
+    // ---- scores, rows [r0-1, r1], columns [28, w-30) in groups of 4 per lane.
+    // Compass survivors go to the wave's ring; full 64-lane rounds drain it.
     const unsigned long long lt = (1ull << lane) - 1;
     const int nsr = r1 - r0 + 2;
+    uint32_t* q = ring[wid];
+    int head = 0, tail = 0;  // wave-uniform
+    auto drain = [&](bool all) {
+        while (tail - head >= 64 || (all && tail > head)) {
+            const int e = head + lane;
+            if (e < tail) {
+                const uint32_t ent = q[e & (kRing - 1)];
+                const int sr = ent >> 12, x = ent & 0xFFF;
+                const uint8_t* row = img + (r0 - 1 + sr - ylo) * SW;
+                const int v = row[x];
+                int c[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) c[k] = row[kCdy[k] * SW + x + kCdx[k]];
+                uint32_t br = 0, dk = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    br |= (uint32_t)(c[k] > v + thr) << k;
+                    dk |= (uint32_t)(c[k] < v - thr) << k;
+                }
+                if (has_run9(br) || has_run9(dk)) sc[sr * SW + x] = (uint8_t)fast_score16(c, v, thr);
+            }
+            head += min(64, tail - head);
+        }
+    };
     for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
         const int y = r0 - 1 + sr;
         const uint8_t* row = img + (y - ylo) * SW;
@@ -302,13 +333,13 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
                 const uint32_t wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
                 const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0);
                 const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
+                const uint32_t ee = __builtin_amdgcn_alignbyte(w1, w0, 3);  // (+3, 0)
+                const uint32_t ww = __builtin_amdgcn_alignbyte(w0, wm, 1);  // (-3, 0)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int v = (w0 >> (8 * j)) & 0xFF;
-                    const int c0 = (dn >> (8 * j)) & 0xFF;        // k = 0: (0, +3)
-                    const int c4 = byte_at(w0, w1, j + 3);       // k = 4: (+3, 0)
-                    const int c8 = (up >> (8 * j)) & 0xFF;        // k = 8: (0, -3)
-                    const int c12 = byte_at(wm, w0, j + 1);      // k = 12: (-3, 0)
+                    const int c0 = (dn >> (8 * j)) & 0xFF, c4 = (ee >> (8 * j)) & 0xFF;
+                    const int c8 = (up >> (8 * j)) & 0xFF, c12 = (ww >> (8 * j)) & 0xFF;
                     const int hi = v + thr, lo = v - thr;
                     const int nb = (c0 > hi) + (c4 > hi) + (c8 > hi) + (c12 > hi);
                     const int nd = (c0 < lo) + (c4 < lo) + (c8 < lo) + (c12 < lo);
@@ -316,66 +347,58 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
                     if ((nb >= 2 || nd >= 2) && x >= 3 && x <= w - 4) cmask |= 1u << j;
                 }
             }
-            int base = 0;
+            const uint32_t ent0 = ((uint32_t)sr << 12) | (uint32_t)x0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const unsigned long long bal = __ballot((cmask >> j) & 1);
-                if ((cmask >> j) & 1) queue[wid][base + __popcll(bal & lt)] = (uint16_t)(x0 + j);
-                base += __popcll(bal);
+                if ((cmask >> j) & 1) q[(tail + __popcll(bal & lt)) & (kRing - 1)] = ent0 + j;
+                tail += __popcll(bal);
             }
-            for (int q = lane; q < base; q += 64) {
-                const int x = queue[wid][q];
-                const int v = row[x];
-                int c[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) c[k] = row[kCdy[k] * SW + x + kCdx[k]];
-                uint32_t br = 0, dk = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    br |= (uint32_t)(c[k] > v + thr) << k;
-                    dk |= (uint32_t)(c[k] < v - thr) << k;
-                }
-                if (has_run9(br) || has_run9(dk)) srow[x] = (uint8_t)fast_score16(c, v, thr);
-            }
+            drain(false);
         }
     }
+    drain(true);
     __syncthreads();
-    // ---- strict 3x3 NMS over rows [r0, r1), columns [31, w-31), raster order
-    auto keep_mask = [&](int y, int x0, uint32_t (&score)[4]) {
-        const uint8_t* s0 = sc + (y - (r0 - 1)) * SW;
-        uint32_t m = 0;
-        if (x0 < w - 31) {
-            const uint32_t a[3][3] = {
-                {*reinterpret_cast<const uint32_t*>(s0 - SW + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 - SW + x0),
-                 *reinterpret_cast<const uint32_t*>(s0 - SW + x0 + 4)},
-                {*reinterpret_cast<const uint32_t*>(s0 + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 + x0),
-                 *reinterpret_cast<const uint32_t*>(s0 + x0 + 4)},
-                {*reinterpret_cast<const uint32_t*>(s0 + SW + x0 - 4), *reinterpret_cast<const uint32_t*>(s0 + SW + x0),
-                 *reinterpret_cast<const uint32_t*>(s0 + SW + x0 + 4)}};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int x = x0 + j;
-                const uint32_t v = byte_at(a[1][1], a[1][2], j);
-                score[j] = v;
-                const uint32_t l0 = j == 0 ? byte_at(a[0][0], a[0][1], 3) : byte_at(a[0][1], a[0][2], j - 1);
-                const uint32_t l1 = j == 0 ? byte_at(a[1][0], a[1][1], 3) : byte_at(a[1][1], a[1][2], j - 1);
-                const uint32_t l2 = j == 0 ? byte_at(a[2][0], a[2][1], 3) : byte_at(a[2][1], a[2][2], j - 1);
-                const uint32_t m0 = byte_at(a[0][1], a[0][2], j), m2 = byte_at(a[2][1], a[2][2], j);
-                const uint32_t q0 = byte_at(a[0][1], a[0][2], j + 1), q1 = byte_at(a[1][1], a[1][2], j + 1),
-                               q2 = byte_at(a[2][1], a[2][2], j + 1);
-                const bool k = x >= kBorder && x < w - kBorder && v > 0 && v > l0 && v > l1 && v > l2 && v > m0 &&
-                               v > m2 && v > q0 && v > q1 && v > q2;
-                m |= (uint32_t)k << j;
-            }
-        }
-        return m;
-    };
+    // ---- strict 3x3 NMS over rows [r0, r1), columns [31, w-31): one pass
+    // stores each lane's 4-bit keep mask (the image strip is free now), counts
+    // per row; after a prefix over rows the keys are written in raster order.
+    uint8_t* kmask = img;
+    const int ngroups = (w - 31 - 28 + 3) >> 2;  // groups x0 = 28 + 4g with x0 < w - 31
     const int nrows = r1 - r0;
     for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
+        const uint8_t* s0 = sc + (rr + 1) * SW;
         int cnt = 0;
-        for (int xb = 28; xb < w - 31; xb += 256) {
-            uint32_t score[4];
-            cnt += __popc(keep_mask(r0 + rr, xb + 4 * lane, score));
+        for (int g = lane; g < ngroups; g += 64) {
+            const int x0 = 28 + 4 * g;
+            uint32_t m = 0;
+            const uint32_t c1 = *reinterpret_cast<const uint32_t*>(s0 + x0);
+            if (c1) {
+                const uint32_t a0 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0 - 4),
+                               a1 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0),
+                               a2 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0 + 4);
+                const uint32_t b0 = *reinterpret_cast<const uint32_t*>(s0 + x0 - 4),
+                               b2 = *reinterpret_cast<const uint32_t*>(s0 + x0 + 4);
+                const uint32_t d0 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0 - 4),
+                               d1 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0),
+                               d2 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0 + 4);
+                // neighbour words shifted by -1 / +1 byte
+                const uint32_t aL = __builtin_amdgcn_alignbyte(a1, a0, 3), aR = __builtin_amdgcn_alignbyte(a2, a1, 1);
+                const uint32_t bL = __builtin_amdgcn_alignbyte(c1, b0, 3), bR = __builtin_amdgcn_alignbyte(b2, c1, 1);
+                const uint32_t dL = __builtin_amdgcn_alignbyte(d1, d0, 3), dR = __builtin_amdgcn_alignbyte(d2, d1, 1);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int sh = 8 * j;
+                    const uint32_t v = (c1 >> sh) & 0xFF;
+                    const uint32_t nmax = max(max(max((aL >> sh) & 0xFF, (a1 >> sh) & 0xFF), max((aR >> sh) & 0xFF,
+                                                                                                  (bL >> sh) & 0xFF)),
+                                              max(max((bR >> sh) & 0xFF, (dL >> sh) & 0xFF),
+                                                  max((d1 >> sh) & 0xFF, (dR >> sh) & 0xFF)));
+                    const int x = x0 + j;
+                    m |= (uint32_t)(v > nmax && x >= kBorder && x < w - kBorder) << j;
+                }
+            }
+            kmask[rr * ngroups + g] = (uint8_t)m;
+            cnt += __popc(m);
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -395,27 +418,25 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)b * G.band_cap;
     for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
         const int y = r0 + rr;
+        const uint8_t* s0 = sc + (rr + 1) * SW;
         int base = row_off[rr];
-        for (int xb = 28; xb < w - 31; xb += 256) {
-            const int x0 = xb + 4 * lane;
-            uint32_t score[4];
-            const uint32_t m = keep_mask(y, x0, score);
-            unsigned long long bal[4];
-            int before = 0;
+        if (row_cnt[rr] == 0) continue;
+        for (int g0 = 0; g0 < ngroups; g0 += 64) {
+            const int g = g0 + lane;
+            const uint32_t m = g < ngroups ? kmask[rr * ngroups + g] : 0u;
+            const int x0 = 28 + 4 * g;
+            const int c = __popc(m);
+            int before = c;  // inclusive scan of c over lanes
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                bal[j] = __ballot((m >> j) & 1);
-                before += __popcll(bal[j] & lt);
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y2 = __shfl_up(before, o);
+                if (lane >= o) before += y2;
             }
-            int mine = 0;
+            int pos = base + before - c;
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if ((m >> j) & 1) {
-                    outp[base + before + mine] = (score[j] << 24) | ((uint32_t)y << 12) | (uint32_t)(x0 + j);
-                    ++mine;
-                }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) base += __popcll(bal[j]);
+                if ((m >> j) & 1) outp[pos++] = ((uint32_t)s0[x0 + j] << 24) | ((uint32_t)y << 12) | (uint32_t)(x0 + j);
+            base += __shfl(before, 63);
         }
     }
 }
