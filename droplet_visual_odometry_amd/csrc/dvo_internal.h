@@ -72,7 +72,7 @@ struct RansacState {
     int32_t best_h, best_i;  // best model: hypothesis, root
     int32_t pad[2];
 };
-constexpr int kRansacRound1 = 256;  // hypotheses per pair in round 1
+constexpr int kRansacRound1 = 128;  // hypotheses per pair in round 1
 
 struct Buffers {
     uint8_t* pyr;

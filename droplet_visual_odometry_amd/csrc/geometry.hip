@@ -557,15 +557,23 @@ __device__ __forceinline__ void dk_sweep(const double (&c)[11], Cx (&roots)[10],
             num = Cx{t.re + c[10 - j - 1], t.im + 0.0};
             if (j != i) {
                 Cx d = csub(p, roots[j]);
-                if (d.re == 0 && d.im == 0) num_same_root++;
-                else denom = cmul(denom, d);
+                if constexpr (kSameRoot) {
+                    if (d.re == 0 && d.im == 0) num_same_root++;
+                    else denom = cmul(denom, d);
+                } else {
+                    denom = cmul(denom, d);  // an exactly zero factor is caught below
+                }
             }
+        }
+        if constexpr (!kSameRoot) {
+            // A coincident root makes a factor exactly 0, so the unconditional
+            // product is 0 or NaN: such polynomials, and the rare false alarms
+            // (underflow, overflow), are redone exactly by the kSameRoot path.
+            same |= !(denom.re != 0 || denom.im != 0) || denom.re != denom.re || denom.im != denom.im;
         }
         num = cdiv(num, denom);
         if constexpr (kSameRoot) {
             if (num_same_root > 1) num = same_root_step(num, num_same_root);
-        } else {
-            same |= num_same_root > 1;
         }
         roots[i] = csub(p, num);
         // std::max(maxDiff, cv::abs(num)) > 0  <=>  re^2 + im^2 > 0 (sqrt is monotone, NaN stays out)
@@ -1030,12 +1038,14 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
         h1 = (S.m > 5 && S.iter < S.niters) ? S.niters : h0;
     }
     const unsigned m = (unsigned)S.m;
+    // x % m by Lemire's fastmod (exact for every 32-bit x and m)
+    const uint64_t M = ~0ull / m + 1;
     Rng rng{S.rng};
     for (int h = h0; h < h1; ++h) {  // getSubset: 5 distinct indices, rng.uniform(0, count)
         int v[5];
         for (int i = 0; i < 5; ++i) {
             for (;;) {
-                v[i] = (int)(rng.next() % m);
+                v[i] = (int)__umul64hi(M * (uint64_t)rng.next(), (uint64_t)m);
                 bool dup = false;
                 for (int j = 0; j < i; ++j) dup |= v[j] == v[i];
                 if (!dup) break;

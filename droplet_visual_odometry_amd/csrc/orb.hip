@@ -818,16 +818,21 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     const uint8_t* center = img + (int64_t)ky * step + kx;
     int m01 = 0, m10 = 0;
     const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
+    const int au = u < 0 ? -u : u;
+    // all 16 row loads of this lane are independent: issue them together
+    int I[16];
+#pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
-        if (v <= 15 && (lane & 31) < 31) {
-            const int av = v < 0 ? -v : v;
-            if ((u < 0 ? -u : u) <= c_umax[av]) {
-                const int I = center[(int64_t)v * step + u];
-                m10 += u * I;
-                m01 += v * I;
-            }
-        }
+        const int av = v < 0 ? -v : v;
+        const bool in = v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av];
+        I[it] = in ? center[(int64_t)v * step + u] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int v = 2 * it + (lane >> 5) - 15;
+        m10 += u * I[it];
+        m01 += v * I[it];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -844,18 +849,20 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     const uint8_t* bl = blur_ptr(P, f, l);
     const int bstep = G.bpitch;
     const uint8_t* bc = bl + (int64_t)cv_round_f(pty * sc) * bstep + cv_round_f(ptx * sc);
-    unsigned long long words[4];
+    int t0[4], t1[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 4; ++q) {  // all 8 gathers first, then the ballots
         const int bit = q * 64 + lane;
         const int px0 = c_pattern[bit * 4 + 0], py0 = c_pattern[bit * 4 + 1];
         const int px1 = c_pattern[bit * 4 + 2], py1 = c_pattern[bit * 4 + 3];
         float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
         float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
-        const int t0 = bc[(int64_t)cv_round_f(y0) * bstep + cv_round_f(x0)];
-        const int t1 = bc[(int64_t)cv_round_f(y1) * bstep + cv_round_f(x1)];
-        words[q] = __ballot(t0 < t1);
+        t0[q] = bc[(int64_t)cv_round_f(y0) * bstep + cv_round_f(x0)];
+        t1[q] = bc[(int64_t)cv_round_f(y1) * bstep + cv_round_f(x1)];
     }
+    unsigned long long words[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) words[q] = __ballot(t0[q] < t1[q]);
     if (lane == 0) {
         dvo_keypoint kp;
         kp.x = ptx;
