@@ -15,7 +15,7 @@
 namespace dvo {
 
 constexpr int kMaxLevels = 8;
-constexpr int kBandRows = 16;       // FAST band height (rows of output per workgroup)
+constexpr int kBandRows = 8;        // FAST band height (rows of output per workgroup)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
 constexpr int kBlurTW = 256, kBlurTH = 32;  // blur tile (4 px x 8 rows per thread)
@@ -72,7 +72,7 @@ struct RansacState {
     int32_t best_h, best_i;  // best model: hypothesis, root
     int32_t pad[2];
 };
-constexpr int kRansacRound1 = 128;  // hypotheses per pair in round 1
+constexpr int kRansacRound1 = 64;   // hypotheses per pair in round 1
 
 struct Buffers {
     uint8_t* pyr;
