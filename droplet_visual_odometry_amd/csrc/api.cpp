@@ -111,12 +111,13 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         const int rows = usable ? G.h - 2 * kBorder : 0;
         const int wc = usable ? G.w - 2 * kBorder : 0;
         G.nbands = (rows + kBandRows - 1) / kBandRows;
+        G.ntx = (wc + kFastTW - 1) / kFastTW;
         G.band_base = bands;
-        bands += G.nbands;
-        G.band_cap = (kBandRows / 2) * ((wc + 1) / 2) + 4;
+        bands += G.nbands * G.ntx;
+        G.band_cap = (kBandRows / 2) * (kFastTW / 2) + 4;  // strict NMS: <= 1 keep per 2x2
         G.band_cand_off = bcand;
-        bcand += (int64_t)G.nbands * G.band_cap;
-        G.cand_cap = G.nbands * G.band_cap + 4;
+        bcand += (int64_t)G.nbands * G.ntx * G.band_cap;
+        G.cand_cap = (kBandRows / 2) * G.nbands * ((wc + 1) / 2) + 4;
         G.cand_off = cand;
         cand += G.cand_cap;
         G.tiles_x = (G.w + kBlurTW - 1) / kBlurTW;
@@ -259,7 +260,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.pyr, (size_t)F * p.pyr_stride);
     A(b.blur, (size_t)F * p.blur_stride);
     A(b.coef, (size_t)std::max(p.coef_total, 1));
-    A(b.band_cnt, (size_t)F * (p.total_bands + 1));
+    A(b.band_cnt, (size_t)F * (p.total_bands + 1) * kBandRows);
     A(b.band_cand, (size_t)F * p.band_cand_stride);
     A(b.cand, (size_t)F * p.cand_stride);
     A(b.resp, (size_t)F * p.cand_stride);

@@ -15,7 +15,8 @@
 namespace dvo {
 
 constexpr int kMaxLevels = 8;
-constexpr int kBandRows = 8;        // FAST band height (rows of output per workgroup)
+constexpr int kBandRows = 16;       // FAST tile height (output rows)
+constexpr int kFastTW = 128;        // FAST tile width (output columns)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
 constexpr int kBlurTW = 256, kBlurTH = 32;  // blur tile (4 px x 8 rows per thread)
@@ -30,10 +31,11 @@ struct LevelGeom {
     int64_t pyr_off;      // byte offset of level l (l >= 1) in a frame's pyramid slab
     int64_t blur_off;     // byte offset of level l in a frame's blurred slab
     int xcoef_off, ycoef_off;  // resize coefficient tables of level l (l >= 1) in Buffers::coef
-    int nbands;           // FAST bands over rows [31, h-31)
-    int band_base;        // first band index of this level within a frame
-    int band_cap;         // candidate capacity per band
-    int64_t band_cand_off;// u32 offset of this level's first band slot within a frame
+    int nbands;           // FAST tile rows (kBandRows each) over rows [31, h-31)
+    int ntx;              // FAST tile columns (kFastTW each) over columns [31, w-31)
+    int band_base;        // first FAST tile of this level within a frame (tile = band * ntx + col)
+    int band_cap;         // candidate capacity per FAST tile
+    int64_t band_cand_off;// u32 offset of this level's first tile slot within a frame
     int cand_cap;         // candidate capacity of the level (>= sum of its band caps)
     int64_t cand_off;     // u32 offset of this level's gathered list within a frame
     int tile_base;        // first blur tile of this level within a frame
@@ -45,7 +47,7 @@ struct Plan {
     LevelGeom L[kMaxLevels];
     int64_t pyr_stride;       // bytes per frame (levels 1..7)
     int64_t blur_stride;      // bytes per frame (levels 0..7)
-    int total_bands;          // per frame
+    int total_bands;          // FAST tiles per frame
     int64_t band_cand_stride; // u32 per frame
     int64_t cand_stride;      // u32 per frame
     int total_tiles;          // blur tiles per frame
@@ -78,7 +80,7 @@ struct Buffers {
     uint8_t* pyr;
     uint8_t* blur;
     int32_t* coef;        // resize coefficient tables (Plan::coef_total ints)
-    int32_t* band_cnt;
+    int32_t* band_cnt;    // [F][total_bands][kBandRows] FAST keeps per tile row
     uint32_t* band_cand;
     uint32_t* cand;       // gathered candidate keys (score<<24 | y<<12 | x)
     float* resp;          // Harris responses parallel to cand

@@ -291,44 +291,49 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
     return k < 4 ? (lo >> (8 * k)) & 0xFF : (hi >> (8 * (k - 4))) & 0xFF;
 }
 
-// One band of kBandRows output rows of one level: the band's image rows (+4
-// halo) are loaded into LDS as words; FAST scores are computed for rows
-// [r0-1, r1] (the NMS neighbourhood).  Every pixel first takes the compass
-// test (a run of 9 on the 16-circle covers >= 2 of the pixels 0, 4, 8, 12),
-// survivors are compacted per wave and only they run the full test + score.
-// Strict 3x3 NMS then emits keys in raster order: per-row counts, a prefix
-// over rows, and within a row ballot ranks in column order.
+// One FAST tile: kBandRows output rows x kFastTW output columns of one level.
+// The tile's image window (+4 rows, +7/+9 columns) is staged in LDS as words;
+// FAST scores are computed for the NMS neighbourhood (rows [r0-1, r1],
+// columns [xs-1, xe]).  Every pixel first takes the compass test (a run of 9
+// on the 16-circle covers >= 2 of the pixels 0, 4, 8, 12); survivors are
+// compacted into a per-wave ring and run the full test + score in full 64-lane
+// rounds.  Strict 3x3 NMS keeps are written per tile row in column order with
+// (offset << 16 | count) per row; select_fast_kernel restores raster order.
+constexpr int kFtLW = kFastTW + 16;  // LDS row: image columns [xs-7, xs+kFastTW+9)
+constexpr int kFtG = kFastTW / 4 + 2;  // 4-pixel groups per row, starting at LDS column 4
 __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int f = blockIdx.y;
     const int item = blockIdx.x;
     int l = 0;
     while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].band_base) ++l;
     const LevelGeom& G = P.plan.L[l];
-    const int b = item - G.band_base;
+    const int t = item - G.band_base;
+    const int b = t / G.ntx, c = t - b * G.ntx;
     const int w = G.w, h = G.h;
     const int r0 = kBorder + b * kBandRows;
     const int r1 = min(r0 + kBandRows, h - kBorder);
+    const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
+    const int bx = xs - 7;  // image column of LDS column 0 (a multiple of 4)
     const int thr = P.plan.fast_threshold;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
-    const int SW = ((w + 3) & ~3) + 16;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* img = smem;                                   // rows [r0-4, r0+kBandRows+4)
-    uint8_t* sc = smem + (kBandRows + 8) * SW;             // rows [r0-1, r0+kBandRows+1)
-    constexpr int kRing = 512;                             // per-wave candidate ring (power of 2)
+    __shared__ __attribute__((aligned(16))) uint8_t img[kBandRows + 8][kFtLW];  // rows [r0-4, r1+4)
+    __shared__ __attribute__((aligned(16))) uint8_t sc[kBandRows + 2][kFtLW];   // rows [r0-1, r1+1)
+    constexpr int kRing = 512;
     __shared__ uint32_t ring[kFastNT / 64][kRing];
-    __shared__ int row_cnt[kBandRows], row_off[kBandRows + 1];
+    __shared__ uint8_t kmask[kBandRows][kFtG + 2];
+    __shared__ int row_cnt[kBandRows];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
-    const int nwords = (w + 3) >> 2;
-    for (int r = 0; r < yhi - ylo; ++r) {
-        const uint32_t* srow = reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp);
-        uint32_t* drow = reinterpret_cast<uint32_t*>(img + r * SW);
-        for (int i = threadIdx.x; i < nwords; i += kFastNT) drow[i] = srow[i];
+    if (threadIdx.x < kBandRows) row_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < (yhi - ylo) * (kFtLW / 4); i += kFastNT) {
+        const int r = i / (kFtLW / 4), wd = i - r * (kFtLW / 4);
+        const int col = bx + 4 * wd;
+        reinterpret_cast<uint32_t*>(img[r])[wd] =
+            col < w ? *reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp + col) : 0u;
     }
     __syncthreads();
-    // ---- scores, rows [r0-1, r1], columns [28, w-30) in groups of 4 per lane.
-    // Compass survivors go to the wave's ring; full 64-lane rounds drain it.
+    // ---- scores: rows [r0-1, r1], groups g in [1, kFtG) (image columns bx + 4g ...)
     const unsigned long long lt = (1ull << lane) - 1;
     const int nsr = r1 - r0 + 2;
     uint32_t* q = ring[wid];
@@ -338,142 +343,126 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
             const int e = head + lane;
             if (e < tail) {
                 const uint32_t ent = q[e & (kRing - 1)];
-                const int sr = ent >> 12, x = ent & 0xFFF;
-                const uint8_t* row = img + (r0 - 1 + sr - ylo) * SW;
-                const int v = row[x];
-                int c[16];
+                const int sr = ent >> 8, lx = ent & 0xFF;
+                const uint8_t* row = &img[sr + 3][lx];
+                const int v = row[0];
+                int cc[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) c[k] = row[kCdy[k] * SW + x + kCdx[k]];
+                for (int k = 0; k < 16; ++k) cc[k] = row[kCdy[k] * kFtLW + kCdx[k]];
                 uint32_t br = 0, dk = 0;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
-                    br |= (uint32_t)(c[k] > v + thr) << k;
-                    dk |= (uint32_t)(c[k] < v - thr) << k;
+                    br |= (uint32_t)(cc[k] > v + thr) << k;
+                    dk |= (uint32_t)(cc[k] < v - thr) << k;
                 }
-                if (has_run9(br) || has_run9(dk)) sc[sr * SW + x] = (uint8_t)fast_score16(c, v, thr);
+                if (has_run9(br) || has_run9(dk)) sc[sr][lx] = (uint8_t)fast_score16(cc, v, thr);
             }
             head += min(64, tail - head);
         }
     };
-    for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
-        const int y = r0 - 1 + sr;
-        const uint8_t* row = img + (y - ylo) * SW;
-        uint8_t* srow = sc + sr * SW;
-        for (int xb = 28; xb < w - 30; xb += 256) {
-            const int x0 = xb + 4 * lane;
-            uint32_t cmask = 0;
-            if (x0 < w - 30) {
-                *reinterpret_cast<uint32_t*>(srow + x0) = 0;
-                const uint32_t up = *reinterpret_cast<const uint32_t*>(row - 3 * SW + x0);
-                const uint32_t dn = *reinterpret_cast<const uint32_t*>(row + 3 * SW + x0);
-                const uint32_t wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
-                const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + x0);
-                const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
-                const uint32_t ee = __builtin_amdgcn_alignbyte(w1, w0, 3);  // (+3, 0)
-                const uint32_t ww = __builtin_amdgcn_alignbyte(w0, wm, 1);  // (-3, 0)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int v = (w0 >> (8 * j)) & 0xFF;
-                    const int c0 = (dn >> (8 * j)) & 0xFF, c4 = (ee >> (8 * j)) & 0xFF;
-                    const int c8 = (up >> (8 * j)) & 0xFF, c12 = (ww >> (8 * j)) & 0xFF;
-                    const int hi = v + thr, lo = v - thr;
-                    const int nb = (c0 > hi) + (c4 > hi) + (c8 > hi) + (c12 > hi);
-                    const int nd = (c0 < lo) + (c4 < lo) + (c8 < lo) + (c12 < lo);
-                    const int x = x0 + j;
-                    if ((nb >= 2 || nd >= 2) && x >= 3 && x <= w - 4) cmask |= 1u << j;
-                }
-            }
-            const uint32_t ent0 = ((uint32_t)sr << 12) | (uint32_t)x0;
+    const int ntask = nsr * (kFtG - 1);
+    for (int t0 = wid * 64; t0 < ntask; t0 += kFastNT) {
+        const int tk = t0 + lane;
+        uint32_t cmask = 0;
+        int sr = 0, lx0 = 0;
+        if (tk < ntask) {
+            sr = tk / (kFtG - 1);
+            lx0 = 4 * (1 + tk - sr * (kFtG - 1));
+            const uint8_t* row = &img[sr + 3][0];
+            *reinterpret_cast<uint32_t*>(&sc[sr][lx0]) = 0;
+            const uint32_t up = *reinterpret_cast<const uint32_t*>(row - 3 * kFtLW + lx0);
+            const uint32_t dn = *reinterpret_cast<const uint32_t*>(row + 3 * kFtLW + lx0);
+            const uint32_t wm = *reinterpret_cast<const uint32_t*>(row + lx0 - 4);
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + lx0);
+            const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + lx0 + 4);
+            const uint32_t ee = __builtin_amdgcn_alignbyte(w1, w0, 3);  // (+3, 0)
+            const uint32_t ww = __builtin_amdgcn_alignbyte(w0, wm, 1);  // (-3, 0)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const unsigned long long bal = __ballot((cmask >> j) & 1);
-                if ((cmask >> j) & 1) q[(tail + __popcll(bal & lt)) & (kRing - 1)] = ent0 + j;
-                tail += __popcll(bal);
+                const int v = (w0 >> (8 * j)) & 0xFF;
+                const int c0 = (dn >> (8 * j)) & 0xFF, c4 = (ee >> (8 * j)) & 0xFF;
+                const int c8 = (up >> (8 * j)) & 0xFF, c12 = (ww >> (8 * j)) & 0xFF;
+                const int hi = v + thr, lo = v - thr;
+                const int nb = (c0 > hi) + (c4 > hi) + (c8 > hi) + (c12 > hi);
+                const int nd = (c0 < lo) + (c4 < lo) + (c8 < lo) + (c12 < lo);
+                const int x = bx + lx0 + j;
+                if ((nb >= 2 || nd >= 2) && x >= xs - 1 && x <= xe && x >= 3 && x <= w - 4) cmask |= 1u << j;
             }
-            drain(false);
         }
+        const uint32_t ent0 = ((uint32_t)sr << 8) | (uint32_t)lx0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned long long bal = __ballot((cmask >> j) & 1);
+            if ((cmask >> j) & 1) q[(tail + __popcll(bal & lt)) & (kRing - 1)] = ent0 + j;
+            tail += __popcll(bal);
+        }
+        drain(false);
     }
     drain(true);
     __syncthreads();
-    // ---- strict 3x3 NMS over rows [r0, r1), columns [31, w-31): one pass
-    // stores each lane's 4-bit keep mask (the image strip is free now), counts
-    // per row; after a prefix over rows the keys are written in raster order.
-    uint8_t* kmask = img;
-    const int ngroups = (w - 31 - 28 + 3) >> 2;  // groups x0 = 28 + 4g with x0 < w - 31
+    // ---- strict 3x3 NMS over rows [r0, r1), columns [xs, xe)
     const int nrows = r1 - r0;
-    for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
-        const uint8_t* s0 = sc + (rr + 1) * SW;
-        int cnt = 0;
-        for (int g = lane; g < ngroups; g += 64) {
-            const int x0 = 28 + 4 * g;
-            uint32_t m = 0;
-            const uint32_t c1 = *reinterpret_cast<const uint32_t*>(s0 + x0);
-            if (c1) {
-                const uint32_t a0 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0 - 4),
-                               a1 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0),
-                               a2 = *reinterpret_cast<const uint32_t*>(s0 - SW + x0 + 4);
-                const uint32_t b0 = *reinterpret_cast<const uint32_t*>(s0 + x0 - 4),
-                               b2 = *reinterpret_cast<const uint32_t*>(s0 + x0 + 4);
-                const uint32_t d0 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0 - 4),
-                               d1 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0),
-                               d2 = *reinterpret_cast<const uint32_t*>(s0 + SW + x0 + 4);
-                // neighbour words shifted by -1 / +1 byte
-                const uint32_t aL = __builtin_amdgcn_alignbyte(a1, a0, 3), aR = __builtin_amdgcn_alignbyte(a2, a1, 1);
-                const uint32_t bL = __builtin_amdgcn_alignbyte(c1, b0, 3), bR = __builtin_amdgcn_alignbyte(b2, c1, 1);
-                const uint32_t dL = __builtin_amdgcn_alignbyte(d1, d0, 3), dR = __builtin_amdgcn_alignbyte(d2, d1, 1);
+    for (int tk = threadIdx.x; tk < nrows * (kFtG - 1); tk += kFastNT) {
+        const int rr = tk / (kFtG - 1), g = 1 + tk - rr * (kFtG - 1);
+        const int lx0 = 4 * g;
+        const uint8_t* s0 = &sc[rr + 1][0];
+        uint32_t m = 0;
+        const uint32_t c1 = *reinterpret_cast<const uint32_t*>(s0 + lx0);
+        if (c1) {
+            const uint32_t a0 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0 - 4),
+                           a1 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0),
+                           a2 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0 + 4);
+            const uint32_t b0 = *reinterpret_cast<const uint32_t*>(s0 + lx0 - 4),
+                           b2 = *reinterpret_cast<const uint32_t*>(s0 + lx0 + 4);
+            const uint32_t d0 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0 - 4),
+                           d1 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0),
+                           d2 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0 + 4);
+            const uint32_t aL = __builtin_amdgcn_alignbyte(a1, a0, 3), aR = __builtin_amdgcn_alignbyte(a2, a1, 1);
+            const uint32_t bL = __builtin_amdgcn_alignbyte(c1, b0, 3), bR = __builtin_amdgcn_alignbyte(b2, c1, 1);
+            const uint32_t dL = __builtin_amdgcn_alignbyte(d1, d0, 3), dR = __builtin_amdgcn_alignbyte(d2, d1, 1);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int sh = 8 * j;
-                    const uint32_t v = (c1 >> sh) & 0xFF;
-                    const uint32_t nmax = max(max(max((aL >> sh) & 0xFF, (a1 >> sh) & 0xFF), max((aR >> sh) & 0xFF,
-                                                                                                  (bL >> sh) & 0xFF)),
-                                              max(max((bR >> sh) & 0xFF, (dL >> sh) & 0xFF),
-                                                  max((d1 >> sh) & 0xFF, (dR >> sh) & 0xFF)));
-                    const int x = x0 + j;
-                    m |= (uint32_t)(v > nmax && x >= kBorder && x < w - kBorder) << j;
-                }
+            for (int j = 0; j < 4; ++j) {
+                const int sh = 8 * j;
+                const uint32_t v = (c1 >> sh) & 0xFF;
+                const uint32_t nmax =
+                    max(max(max((aL >> sh) & 0xFF, (a1 >> sh) & 0xFF), max((aR >> sh) & 0xFF, (bL >> sh) & 0xFF)),
+                        max(max((bR >> sh) & 0xFF, (dL >> sh) & 0xFF), max((d1 >> sh) & 0xFF, (dR >> sh) & 0xFF)));
+                const int x = bx + lx0 + j;
+                m |= (uint32_t)(v > nmax && x >= xs && x < xe) << j;
             }
-            kmask[rr * ngroups + g] = (uint8_t)m;
-            cnt += __popc(m);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-        if (lane == 0) row_cnt[rr] = cnt;
+        kmask[rr][g] = (uint8_t)m;
+        if (m) atomicAdd(&row_cnt[rr], __popc(m));
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int rr = 0; rr < nrows; ++rr) {
-            row_off[rr] = acc;
-            acc += row_cnt[rr];
-        }
-        row_off[nrows] = acc;
-        P.buf.band_cnt[(int64_t)f * P.plan.total_bands + item] = acc;
+    uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)t * G.band_cap;
+    int32_t* cnt_out = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + item) * kBandRows;
+    if (threadIdx.x < kBandRows) {
+        int off = 0;
+        for (int rr = 0; rr < threadIdx.x; ++rr) off += row_cnt[rr];
+        cnt_out[threadIdx.x] = threadIdx.x < nrows ? (off << 16) | row_cnt[threadIdx.x] : 0;
     }
-    __syncthreads();
-    uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)b * G.band_cap;
     for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
-        const int y = r0 + rr;
-        const uint8_t* s0 = sc + (rr + 1) * SW;
-        int base = row_off[rr];
         if (row_cnt[rr] == 0) continue;
-        for (int g0 = 0; g0 < ngroups; g0 += 64) {
-            const int g = g0 + lane;
-            const uint32_t m = g < ngroups ? kmask[rr * ngroups + g] : 0u;
-            const int x0 = 28 + 4 * g;
-            const int c = __popc(m);
-            int before = c;  // inclusive scan of c over lanes
+        int off = 0;
+        for (int k = 0; k < rr; ++k) off += row_cnt[k];
+        const int g = 1 + lane;
+        const uint32_t m = g < kFtG ? kmask[rr][g] : 0u;
+        const int cm = __popc(m);
+        int incl = cm;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y2 = __shfl_up(before, o);
-                if (lane >= o) before += y2;
-            }
-            int pos = base + before - c;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((m >> j) & 1) outp[pos++] = ((uint32_t)s0[x0 + j] << 24) | ((uint32_t)y << 12) | (uint32_t)(x0 + j);
-            base += __shfl(before, 63);
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y2 = __shfl_up(incl, o);
+            if (lane >= o) incl += y2;
         }
+        int pos = off + incl - cm;
+        const int y = r0 + rr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((m >> j) & 1) {
+                const int lx = 4 * g + j;
+                outp[pos++] = ((uint32_t)sc[rr + 1][lx] << 24) | ((uint32_t)y << 12) | (uint32_t)(bx + lx);
+            }
     }
 }
 
@@ -731,24 +720,34 @@ __global__ __launch_bounds__(kSelNT) void select_fast_kernel(StreamParams P) {
     if (l >= P.plan.nlevels) return;
     const LevelGeom& G = P.plan.L[l];
     __shared__ int lds[64];
-    __shared__ int boff[1024 + 1];
-    const int32_t* bc = P.buf.band_cnt + (int64_t)f * P.plan.total_bands + G.band_base;
+    __shared__ int s_carry;
+    const int32_t* rc = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + G.band_base) * kBandRows;
     const uint32_t* bsrc = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off;
     uint32_t* A = P.buf.cand + (int64_t)f * P.plan.cand_stride + G.cand_off;
-    if (threadIdx.x == 0) {
-        int s = 0;
-        for (int b = 0; b < G.nbands; ++b) {
-            boff[b] = s;
-            s += bc[b];
-        }
-        boff[G.nbands] = s;
-    }
+    // raster order: segment (band b, row rr, tile column c) = s = (b * kBandRows + rr) * ntx + c
+    const int nseg = G.nbands * kBandRows * G.ntx;
+    if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
-    const int n = boff[G.nbands];
-    for (int b = 0; b < G.nbands; ++b) {
-        const int c = boff[b + 1] - boff[b];
-        for (int i = threadIdx.x; i < c; i += kSelNT) A[boff[b] + i] = bsrc[(int64_t)b * G.band_cap + i];
+    for (int s0 = 0; s0 < nseg; s0 += kSelNT) {
+        const int sg = s0 + threadIdx.x;
+        int cnt = 0, src_off = 0;
+        if (sg < nseg) {
+            const int cc = sg % G.ntx, br = sg / G.ntx;
+            const int b = br / kBandRows, rr = br - b * kBandRows;
+            const int tile = b * G.ntx + cc;
+            const int v = rc[(int64_t)tile * kBandRows + rr];
+            cnt = v & 0xFFFF;
+            src_off = tile * G.band_cap + (v >> 16);
+        }
+        int tot;
+        const int off = block_excl_scan(cnt, tot, lds);
+        const int base = s_carry;
+        for (int i = 0; i < cnt; ++i) A[base + off + i] = bsrc[src_off + i];
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = base + tot;
+        __syncthreads();
     }
+    const int n = s_carry;
     __syncthreads();
     int32_t* Lpos = P.buf.sel_tmp + (int64_t)f * 2 * P.plan.cand_stride + 2 * G.cand_off;
     int32_t* Rasc = Lpos + G.cand_cap;
@@ -938,11 +937,10 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     mark(ev, 1, 0, s);
     hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles, F), dim3(256), 0, s, P);
     mark(ev, 1, 1, s);
-    const int SW = ((pl.L[0].w + 3) & ~3) + 16;
-    const size_t fast_lds = (size_t)(2 * kBandRows + 10) * SW;
+
     mark(ev, 2, 0, s);
     if (pl.total_bands > 0)
-        hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), fast_lds, s, P);
+        hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
