@@ -89,6 +89,100 @@ __global__ __launch_bounds__(kNNThreads) void nn_stream_kernel(StreamParams P) {
     nn_block(J, qbase, lds);
 }
 
+// Fused forward + backward nearest neighbours of one stream pair: every
+// distance is computed once.  A block owns 1024 queries of frame p (4 per
+// lane); the trains of frame p+1 stream through LDS.  Each wave takes 64
+// trains per pass (one per lane) and rotates them around the wave with DPP
+// wave_ror:1 for 64 rounds, so every lane meets every train; the row minimum
+// (forward NN) stays in the lane, the column minimum (backward NN) travels
+// with its train and is folded into LDS, then global, with atomicMin on packed
+// (distance << 16 | index) keys, which keeps OpenCV's first-index tie rule.
+constexpr int kFQ = 4, kFNT = 256, kFQB = kFQ * kFNT, kFChunk = 1024;
+
+__device__ __forceinline__ uint32_t ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);  // wave_ror:1
+}
+
+__global__ __launch_bounds__(kFNT) void nn_fused_kernel(StreamParams P) {
+    __shared__ uint4 lds[kFChunk * 2];
+    __shared__ int colmin[kFChunk];
+    const int p = blockIdx.y;
+    const int nq = min(P.buf.nkp[p], P.plan.kp_cap), nt = min(P.buf.nkp[p + 1], P.plan.kp_cap);
+    const int qbase = blockIdx.x * kFQB;
+    if (qbase >= nq) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint4* qg = reinterpret_cast<const uint4*>(P.buf.desc + (int64_t)p * P.plan.kp_cap * 32);
+    const uint4* tg = reinterpret_cast<const uint4*>(P.buf.desc + (int64_t)(p + 1) * P.plan.kp_cap * 32);
+    int32_t* fwd = P.buf.nn + (int64_t)p * P.plan.kp_cap;
+    int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * P.plan.kp_cap;
+    uint4 qa[kFQ][2];
+    int best[kFQ], qkey[kFQ];
+#pragma unroll
+    for (int r = 0; r < kFQ; ++r) {
+        const int q = qbase + (wid * kFQ + r) * 64 + lane;
+        best[r] = 0x7FFFFFFF;
+        qkey[r] = q < nq ? q : 0x7FFFFFFF;  // invalid queries never win a column
+        if (q < nq) {
+            qa[r][0] = qg[2 * q];
+            qa[r][1] = qg[2 * q + 1];
+        } else {
+            qa[r][0] = make_uint4(0, 0, 0, 0);
+            qa[r][1] = make_uint4(0, 0, 0, 0);
+        }
+    }
+    for (int t0 = 0; t0 < nt; t0 += kFChunk) {
+        const int nc = min(kFChunk, nt - t0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < nc * 2; i += kFNT) lds[i] = tg[2 * t0 + i];
+        for (int i = threadIdx.x; i < nc; i += kFNT) colmin[i] = 0x7FFFFFFF;
+        __syncthreads();
+        for (int pass = 0; pass < nc; pass += 64) {
+            const int tt = pass + lane;
+            uint4 a, b;
+            if (tt < nc) {
+                a = lds[2 * tt];
+                b = lds[2 * tt + 1];
+            } else {
+                a = make_uint4(0, 0, 0, 0);
+                b = make_uint4(0, 0, 0, 0);
+            }
+            uint32_t tid = tt < nc ? (uint32_t)(t0 + tt) : 0xFFFFu;  // travels with the train
+            int cmin = 0x7FFFFFFF;
+            for (int r = 0; r < 64; ++r) {
+                const bool tv = tid != 0xFFFFu;
+#pragma unroll
+                for (int j = 0; j < kFQ; ++j) {
+                    const int d = __popc(a.x ^ qa[j][0].x) + __popc(a.y ^ qa[j][0].y) + __popc(a.z ^ qa[j][0].z) +
+                                  __popc(a.w ^ qa[j][0].w) + __popc(b.x ^ qa[j][1].x) + __popc(b.y ^ qa[j][1].y) +
+                                  __popc(b.z ^ qa[j][1].z) + __popc(b.w ^ qa[j][1].w);
+                    if (tv) best[j] = min(best[j], (d << 16) | (int)tid);
+                    cmin = min(cmin, qkey[j] == 0x7FFFFFFF ? 0x7FFFFFFF : (d << 16) | qkey[j]);
+                }
+                a.x = ror1(a.x);
+                a.y = ror1(a.y);
+                a.z = ror1(a.z);
+                a.w = ror1(a.w);
+                b.x = ror1(b.x);
+                b.y = ror1(b.y);
+                b.z = ror1(b.z);
+                b.w = ror1(b.w);
+                tid = ror1(tid);
+                cmin = (int)ror1((uint32_t)cmin);
+            }
+            // after 64 rotations every train is back in its home lane
+            if (tt < nc) atomicMin(&colmin[tt], cmin);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nc; i += kFNT)
+            if (colmin[i] != 0x7FFFFFFF) atomicMin(&bwd[t0 + i], colmin[i]);
+    }
+#pragma unroll
+    for (int r = 0; r < kFQ; ++r) {
+        const int q = qbase + (wid * kFQ + r) * 64 + lane;
+        if (q < nq) fwd[q] = nt > 0 ? best[r] : -1;
+    }
+}
+
 __global__ __launch_bounds__(kNNThreads) void nn_pair_kernel(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                              int32_t* out) {
     extern __shared__ uint4 lds[];
@@ -116,7 +210,7 @@ __device__ int crosscheck_sort(const int32_t* fwd, const int32_t* bwd, int nq, i
         __syncthreads();
         for (int t = threadIdx.x; t < nt; t += kXNT) {
             int b = bwd[t];
-            if (b < 0) continue;
+            if (b < 0 || (b >> 16) > 256) continue;  // -1 or the untouched 0x7F7F7F7F fill
             int q = b & 0xFFFF, d = b >> 16;
             atomicMin(&keys[q], ((uint32_t)d << 16) | (uint32_t)t);
         }
@@ -247,9 +341,10 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     if (P.nframes < 2) return hipSuccess;
     mark(ev, 5, 0, s);
     const int cap = P.plan.kp_cap;
-    const size_t lds = (size_t)(cap < kTrainChunk ? cap : kTrainChunk) * 32;
-    dim3 grid((cap + kNNQ - 1) / kNNQ, 2, P.nframes - 1);
-    hipLaunchKernelGGL(nn_stream_kernel, grid, dim3(kNNThreads), lds, s, P);
+    // backward keys start at 0x7F7F7F7F ("none") and are lowered by atomicMin
+    hipError_t e = hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F, sizeof(int32_t) * (size_t)P.nframes * cap, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(nn_fused_kernel, dim3((cap + kFQB - 1) / kFQB, P.nframes - 1), dim3(kFNT), 0, s, P);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();

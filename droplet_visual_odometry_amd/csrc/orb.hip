@@ -826,7 +826,13 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // One wave per keypoint: ICAngles (integer moments, wave-reduced), then
 // pt *= scale, size = 31*scale, and the 256 rBRIEF bits — lane j evaluates bits
 // j, j+64, j+128, j+192 and a ballot assembles each 64-bit descriptor word.
+// One wave per keypoint.  Everything the keypoint needs is requested at once:
+// the 16 IC-angle row segments of the unblurred level (registers) and the
+// blurred 39 x 44 window around it (word loads into LDS); the 512 rBRIEF
+// samples are then LDS reads.
+constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
+    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kDPH][kDPW];
     const int f = blockIdx.y;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int k = blockIdx.x * 4 + wv;
@@ -837,32 +843,53 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         P.buf.nkp[f] = total;
         if (total > P.plan.kp_cap) atomicOr(&P.buf.status[f], 1);
     }
-    if (k >= total || k >= P.plan.kp_cap) return;
-    int l = 0, i = k;
-    while (i >= c2[l]) {
+    if (blockIdx.x * 4 >= min(total, P.plan.kp_cap)) return;  // whole block idle (uniform)
+    const bool valid = k < total && k < P.plan.kp_cap;
+    int l = 0, i = valid ? k : 0;
+    while (l + 1 < P.plan.nlevels && i >= c2[l]) {
         i -= c2[l];
         ++l;
     }
     const LevelGeom& G = P.plan.L[l];
-    const uint32_t key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
-    const float response = P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+    uint32_t key = 0;
+    float response = 0.f;
+    if (valid) {
+        key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+        response = P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
+    }
     const int kx = key & 0xFFF, ky = (key >> 12) & 0xFFF;
-    // ---- ICAngles on the unblurred level
-    const uint8_t* img = level_ptr(P, f, l);
-    const int step = level_pitch(P, l);
-    const uint8_t* center = img + (int64_t)ky * step + kx;
-    int m01 = 0, m10 = 0;
+    const float scale = G.scale;
+    const float ptx = (float)kx * scale, pty = (float)ky * scale;
+    const float sc = 1.f / scale;
+    const int cxb = cv_round_f(ptx * sc), cyb = cv_round_f(pty * sc);  // orb.cpp: center = &img(cvRound(pt*sc))
     const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
     const int au = u < 0 ? -u : u;
-    // all 16 row loads of this lane are independent: issue them together
     int I[16];
+    const int a0 = (cxb - kDPR) & ~3;
+    if (valid) {
+        // ---- ICAngles rows (unblurred level), all 16 loads in flight
+        const uint8_t* img = level_ptr(P, f, l);
+        const int step = level_pitch(P, l);
+        const uint8_t* center = img + (int64_t)ky * step + kx;
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
-        const int av = v < 0 ? -v : v;
-        const bool in = v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av];
-        I[it] = in ? center[(int64_t)v * step + u] : 0;
+        for (int it = 0; it < 16; ++it) {
+            const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
+            const int av = v < 0 ? -v : v;
+            const bool in = v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av];
+            I[it] = in ? center[(int64_t)v * step + u] : 0;
+        }
+        // ---- blurred window rows cyb-19 .. cyb+19, words from a0
+        const uint8_t* bl = blur_ptr(P, f, l);
+        const int bstep = G.bpitch;
+        for (int e = lane; e < kDPH * (kDPW / 4); e += 64) {
+            const int r = e / (kDPW / 4), wd = e - r * (kDPW / 4);
+            reinterpret_cast<uint32_t*>(patch[wv][r])[wd] =
+                *reinterpret_cast<const uint32_t*>(bl + (int64_t)(cyb - kDPR + r) * bstep + a0 + 4 * wd);
+        }
     }
+    __syncthreads();
+    if (!valid) return;
+    int m01 = 0, m10 = 0;
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int v = 2 * it + (lane >> 5) - 15;
@@ -875,25 +902,20 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         m01 += __shfl_xor(m01, o);
     }
     const float angle = fast_atan2((float)m01, (float)m10);
-    const float scale = G.scale;
-    const float ptx = (float)kx * scale, pty = (float)ky * scale;
     // ---- rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
-    const float sc = 1.f / scale;
     const float ang = angle * (float)(M_PI / 180.f);
     const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
-    const uint8_t* bl = blur_ptr(P, f, l);
-    const int bstep = G.bpitch;
-    const uint8_t* bc = bl + (int64_t)cv_round_f(pty * sc) * bstep + cv_round_f(ptx * sc);
+    const uint8_t* pc = &patch[wv][kDPR][cxb - a0];
     int t0[4], t1[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // all 8 gathers first, then the ballots
+    for (int q = 0; q < 4; ++q) {
         const int bit = q * 64 + lane;
         const int px0 = c_pattern[bit * 4 + 0], py0 = c_pattern[bit * 4 + 1];
         const int px1 = c_pattern[bit * 4 + 2], py1 = c_pattern[bit * 4 + 3];
         float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
         float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
-        t0[q] = bc[(int64_t)cv_round_f(y0) * bstep + cv_round_f(x0)];
-        t1[q] = bc[(int64_t)cv_round_f(y1) * bstep + cv_round_f(x1)];
+        t0[q] = pc[cv_round_f(y0) * kDPW + cv_round_f(x0)];
+        t1[q] = pc[cv_round_f(y1) * kDPW + cv_round_f(x1)];
     }
     unsigned long long words[4];
 #pragma unroll
