@@ -176,12 +176,16 @@ def main():
     if stage_ms and calls:
         sb = stage_bytes(W, H, N, m_avg)
         per_call = {k: v / calls for k, v in stage_ms.items()}
-        dom = max(per_call, key=per_call.get)
-        frames_per_call = B + 1 if dom in ("pyramid", "blur", "fast", "select_harris", "describe") else B
-        bytes_per_launch = sb[dom] * frames_per_call
+        # roofline of the dominant single-kernel stage (one launch per step, so the
+        # HIP-event time on the library's stream is that kernel's duration)
+        single = {"fast": "fast_band_kernel", "blur": "blur_kernel", "describe": "describe_kernel"}
+        dom = max(single, key=lambda k: per_call.get(k, 0.0))
+        bytes_per_launch = sb[dom] * (B + 1)
         achieved = bytes_per_launch / (per_call[dom] * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(single[dom], W, H, N, B)
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None, "kernel": dom,
+                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": single[dom], "algorithmic_bytes_per_launch": bytes_per_launch,
                     "kernel_ms_per_launch": round(per_call[dom], 4),
                     "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
                     "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
@@ -189,8 +193,27 @@ def main():
                                        / HBM_PEAK_GBS, 8)}
 
     cpu = None
+    pose_check = None
     if args.cpu_seconds > 0 and world == 1:
-        cpu = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds)
+        cpu, ref = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds)
+        # the same pairs on the GPU (window 0), compared with the oracle's R, t
+        fss[0].process(pool[0:B + 1], recs_t[0], wait_torch=False)
+        fss[0].sync()
+        g = FrameStream.records_numpy(recs_t[0], B)
+        n = min(len(ref), B)
+        ident = 0
+        err_r = err_t = 0.0
+        for i in range(n):
+            R_ref, t_ref = ref[i]
+            if R_ref is None:
+                ident += int(g["status"][i] != 0)
+                continue
+            Rg, tg = g["R"][i].reshape(3, 3), g["t"][i]
+            ident += int(np.array_equal(Rg, R_ref) and np.array_equal(tg, t_ref.ravel()))
+            err_r = max(err_r, float(np.max(np.abs(Rg - R_ref))))
+            err_t = max(err_t, float(np.max(np.abs(tg - t_ref.ravel()))))
+        pose_check = {"pairs": n, "bit_identical": ident, "max_abs_R_err": err_r, "max_abs_t_err": err_t,
+                      "reference": "oracle/ C++ restatement, same frames"}
 
     out = {
         "metric": "frames/sec (detect+match+pose) at 1280x720, 2000 feats",
@@ -213,10 +236,27 @@ def main():
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "pose_check": pose_check,
     }
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, W, H, N, B):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/r01_pmc_traffic.json: FETCH_SIZE + WRITE_SIZE), when they were
+    taken on this configuration; PMC counters cannot run inside the timed loop."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    c = doc.get("config", {})
+    k = doc.get("kernels", {}).get(kernel)
+    if k is None or (c.get("width"), c.get("height"), c.get("nfeatures"), c.get("batch")) != (W, H, N, B):
+        return None, None
+    return round(k["fetch_bytes"] + k["write_bytes"]), "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"
 
 
 def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
@@ -225,20 +265,23 @@ def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
-    frames = pool.cpu().numpy()
     t0 = time.perf_counter()
-    kp_prev = oracle.detect_and_compute(frames[0], nfeatures)
+    kp_prev = oracle.detect_and_compute(pool[0].cpu().numpy(), nfeatures)
     n = 0
     i = 0
-    while time.perf_counter() - t0 < seconds and i + 1 < len(frames):
-        r = oracle.pair_pose(frames[i], frames[i + 1], K, nfeatures, max_iters=max_iters, kp_prev=kp_prev)
+    ref = []
+    while time.perf_counter() - t0 < seconds and i + 1 < len(pool):
+        a, b = pool[i].cpu().numpy(), pool[i + 1].cpu().numpy()
+        r = oracle.pair_pose(a, b, K, nfeatures, max_iters=max_iters, kp_prev=kp_prev)
         kp_prev = (r["kp_cur"], r["desc_cur"])
+        ref.append((r["R"], r["t_unit"]))
         n += 1
         i += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} consecutive pairs of the same 1280x720 stream ({dt:.1f} s, first frame's detect "
-                      f"included), oracle/ C++ restatement of the OpenCV path, streaming mode"}
+    return ({"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+             "sample": f"{n} consecutive pairs of the same {pool.shape[2]}x{pool.shape[1]} stream ({dt:.1f} s, "
+                       f"first frame's detect included), oracle/ C++ restatement of the OpenCV path, streaming "
+                       f"mode, one host core"}, ref)
 
 
 if __name__ == "__main__":
