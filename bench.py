@@ -80,10 +80,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # DVO_BENCH_BACKEND=gloo: rehearsal of the multi-rank path on fewer GPUs than
+    # ranks (ranks share devices, records are gathered through host memory).
+    backend = os.environ.get("DVO_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local_rank = local_rank % torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if backend == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
 
     from droplet_visual_odometry_amd._native import Context, PAIR_RECORD_DTYPE
@@ -112,7 +120,8 @@ def main():
     T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     fss[0].reset_pose()
     torch.cuda.synchronize()
-    gathered = [torch.empty(world * recs_t[0].numel(), dtype=torch.uint8, device=dev) for _ in range(S)] \
+    gdev = torch.device("cpu") if backend == "gloo" else dev
+    gathered = [torch.empty(world * recs_t[0].numel(), dtype=torch.uint8, device=gdev) for _ in range(S)] \
         if world > 1 else None
     n_windows = max(1, (pool_n - 1) // B)
 
@@ -123,9 +132,13 @@ def main():
         fs.process(pool[s:s + B + 1], recs_t[k], wait_torch=False)
         fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
         if world > 1:
-            # RCCL (on torch's stream) reads the records once the library's stream has written them
-            torch.cuda.current_stream().wait_event(fs.record_event())
-            dist.all_gather_into_tensor(gathered[k], recs_t[k])
+            if backend == "gloo":
+                fs.sync()
+                dist.all_gather_into_tensor(gathered[k], recs_t[k].cpu())
+            else:
+                # RCCL (on torch's stream) reads the records once the library's stream has written them
+                torch.cuda.current_stream().wait_event(fs.record_event())
+                dist.all_gather_into_tensor(gathered[k], recs_t[k])
 
     def sync_all():
         for f in fss:
@@ -149,7 +162,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -230,7 +243,9 @@ def main():
         "data": "synthetic (seeded ray-cast textured room, droplet_visual_odometry_amd/synth.py)",
         "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, batch {B} new frames/step per GPU",
                    "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
-                   "parallelism": f"frame-sharded x{world}" + (" + RCCL all_gather" if world > 1 else ""),
+                   "parallelism": f"frame-sharded x{world}" + (
+                       (" + RCCL all_gather" if backend != "gloo" else " + gloo all_gather (rehearsal)")
+                       if world > 1 else ""),
                    "streams_in_flight": S,
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},

@@ -20,9 +20,11 @@ from ._native import (DMATCH_DTYPE, KEYPOINT_DTYPE, PAIR_RECORD_DTYPE, Context, 
 class FrameStream:
     def __init__(self, width: int, height: int, K, nfeatures: int = 500, max_frames: int = 64, prob: float = 0.999,
                  threshold: float = 1.0, max_iters: int = 1000, cross_check: int = 1, dist_thresh: float = 50.0,
-                 device: int = 0, ctx: Context | None = None):
-        self.ctx = ctx if ctx is not None else Context(device)
-        self.device = torch.device("cuda", device)
+                 device: int | None = None, ctx: Context | None = None):
+        if ctx is not None and device is not None and device != ctx.device:
+            raise ValueError(f"device {device} != context device {ctx.device}")
+        self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
+        self.device = torch.device("cuda", self.ctx.device)  # the library runs on the context's device
         cfg = StreamConfig()
         cfg.width, cfg.height, cfg.max_frames = int(width), int(height), int(max_frames)
         cfg.orb = orb_params(nfeatures=nfeatures)
