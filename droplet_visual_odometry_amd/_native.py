@@ -90,6 +90,13 @@ _SIGNATURES = {
     "dvo_stream_hip_stream": ([_vp], _vp),
     "dvo_stream_set_profiling": ([_vp, _c], _c),
     "dvo_stream_reset_pose": ([_vp, _vp, _vp], _c),
+    "dvo_get_optimal_new_camera_matrix": ([_vp, _vp, _c, _c, _c, _d, _c, _c, _vp], _c),
+    "dvo_undistort_create": ([_vp, _vp, _vp, _c, _vp, _c, _c, _vp], _c),
+    "dvo_undistort_destroy": ([_vp], None),
+    "dvo_undistort_apply": ([_vp, _vp, _c, ctypes.c_int64, _c, _vp, ctypes.c_int64, _c, _vp], _c),
+    "dvo_undistort_image": ([_vp, _vp, _c, _vp, _c], _c),
+    "dvo_undistort_get_map": ([_vp, _vp, _vp], _c),
+    "dvo_stream_process_undistorted": ([_vp, _vp, _vp, _c, _i64, _c, _vp], _c),
     "dvo_stream_share_pose": ([_vp, _vp], _c),
     "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),

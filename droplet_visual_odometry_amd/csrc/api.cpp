@@ -4,6 +4,8 @@
 // HIP kernels of orb.hip, match.hip and geometry.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -882,3 +884,237 @@ int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Image pre-processing: cv.getOptimalNewCameraMatrix / cv.undistort
+// (visual_odometry_v3.py:110-135).
+namespace {
+
+int load_dist12(dvo_ctx* ctx, const double* dist, int ndist, double* k) {
+    for (int i = 0; i < 12; ++i) k[i] = 0.0;
+    if (ndist < 0 || (ndist > 0 && !dist)) return fail(ctx, DVO_EINVAL, "bad distortion coefficients");
+    if (!(ndist == 0 || ndist == 4 || ndist == 5 || ndist == 8 || ndist == 12))
+        return fail(ctx, DVO_EINVAL, "distortion must have 4, 5, 8 or 12 coefficients (tilt models unsupported)");
+    for (int i = 0; i < ndist; ++i) k[i] = dist[i];
+    return DVO_OK;
+}
+
+// undistort.dispatch.cpp cvUndistortPointsInternal (R = P = I, 5 iterations),
+// float points in and out.
+void undistort_points_f(float* pts, int n, const double* A, const double* k) {
+    const double fx = A[0], fy = A[4], ifx = 1. / fx, ify = 1. / fy, cx = A[2], cy = A[5];
+    for (int i = 0; i < n; ++i) {
+        double x = pts[2 * i], y = pts[2 * i + 1];
+        const double u = x, v = y;
+        x = (x - cx) * ifx;
+        y = (y - cy) * ify;
+        const double x0 = x, y0 = y;
+        for (int j = 0; j < 5; ++j) {
+            const double r2 = x * x + y * y;
+            const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+            if (icdist < 0) {
+                x = (u - cx) * ifx;
+                y = (v - cy) * ify;
+                break;
+            }
+            const double dx = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+            const double dy = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+            x = (x0 - dx) * icdist;
+            y = (y0 - dy) * icdist;
+        }
+        const double ww = 1. / (0. * x + 0. * y + 1.);
+        pts[2 * i] = (float)((1. * x + 0. * y + 0.) * ww);
+        pts[2 * i + 1] = (float)((0. * x + 1. * y + 0.) * ww);
+    }
+}
+
+// Mat::inv(DECOMP_LU) of a 3x3 (LU with partial pivoting on [A | I]).
+bool inv3(const double* M, double* out) {
+    double A[9], b[9];
+    std::memcpy(A, M, sizeof(A));
+    for (int i = 0; i < 9; ++i) b[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int i = 0; i < 3; i++) {
+        int k = i;
+        for (int j = i + 1; j < 3; j++)
+            if (std::fabs(A[j * 3 + i]) > std::fabs(A[k * 3 + i])) k = j;
+        if (std::fabs(A[k * 3 + i]) < DBL_EPSILON * 100) return false;
+        if (k != i) {
+            for (int j = i; j < 3; j++) std::swap(A[i * 3 + j], A[k * 3 + j]);
+            for (int j = 0; j < 3; j++) std::swap(b[i * 3 + j], b[k * 3 + j]);
+        }
+        const double d = -1 / A[i * 3 + i];
+        for (int j = i + 1; j < 3; j++) {
+            const double alpha = A[j * 3 + i] * d;
+            for (int c = i + 1; c < 3; c++) A[j * 3 + c] += alpha * A[i * 3 + c];
+            for (int c = 0; c < 3; c++) b[j * 3 + c] += alpha * b[i * 3 + c];
+        }
+    }
+    for (int i = 2; i >= 0; i--)
+        for (int j = 0; j < 3; j++) {
+            double s = b[i * 3 + j];
+            for (int k = i + 1; k < 3; k++) s -= A[i * 3 + k] * b[k * 3 + j];
+            b[i * 3 + j] = s / A[i * 3 + i];
+        }
+    std::memcpy(out, b, sizeof(b));
+    return true;
+}
+
+}  // namespace
+
+struct dvo_undistort {
+    dvo_ctx* ctx = nullptr;
+    UndistortGeom U{};
+    double* d_ir = nullptr;
+    int16_t* d_xy = nullptr;
+    uint16_t* d_frac = nullptr;
+};
+
+int dvo_get_optimal_new_camera_matrix(const double* K, const double* dist, int ndist, int w, int h, double alpha,
+                                      int new_w, int new_h, double* newK) {
+    if (!K || !newK || w <= 0 || h <= 0) return DVO_EINVAL;
+    double k[12];
+    if (load_dist12(nullptr, dist, ndist, k)) return DVO_EINVAL;
+    if (new_w * new_h == 0) {
+        new_w = w;
+        new_h = h;
+    }
+    // calibration.cpp icvGetRectangles: a 9 x 9 grid over the image, undistorted
+    const int N = 9;
+    float pts[2 * N * N];
+    for (int y = 0, i = 0; y < N; y++)
+        for (int x = 0; x < N; x++, i++) {
+            pts[2 * i] = (float)x * w / (N - 1);
+            pts[2 * i + 1] = (float)y * h / (N - 1);
+        }
+    undistort_points_f(pts, N * N, K, k);
+    float iX0 = -FLT_MAX, iX1 = FLT_MAX, iY0 = -FLT_MAX, iY1 = FLT_MAX;
+    float oX0 = FLT_MAX, oX1 = -FLT_MAX, oY0 = FLT_MAX, oY1 = -FLT_MAX;
+    for (int y = 0, i = 0; y < N; y++)
+        for (int x = 0; x < N; x++, i++) {
+            const float px = pts[2 * i], py = pts[2 * i + 1];
+            oX0 = std::min(oX0, px);
+            oX1 = std::max(oX1, px);
+            oY0 = std::min(oY0, py);
+            oY1 = std::max(oY1, py);
+            if (x == 0) iX0 = std::max(iX0, px);
+            if (x == N - 1) iX1 = std::min(iX1, px);
+            if (y == 0) iY0 = std::max(iY0, py);
+            if (y == N - 1) iY1 = std::min(iY1, py);
+        }
+    const float in_w = iX1 - iX0, in_h = iY1 - iY0, ou_w = oX1 - oX0, ou_h = oY1 - oY0;
+    std::memcpy(newK, K, 9 * sizeof(double));
+    const double fx0 = (new_w - 1) / in_w, fy0 = (new_h - 1) / in_h, cx0 = -fx0 * iX0, cy0 = -fy0 * iY0;
+    const double fx1 = (new_w - 1) / ou_w, fy1 = (new_h - 1) / ou_h, cx1 = -fx1 * oX0, cy1 = -fy1 * oY0;
+    newK[0] = fx0 * (1 - alpha) + fx1 * alpha;
+    newK[4] = fy0 * (1 - alpha) + fy1 * alpha;
+    newK[2] = cx0 * (1 - alpha) + cx1 * alpha;
+    newK[5] = cy0 * (1 - alpha) + cy1 * alpha;
+    return DVO_OK;
+}
+
+int dvo_undistort_create(dvo_ctx* ctx, const double* K, const double* dist, int ndist, const double* newK, int w,
+                         int h, dvo_undistort** out) {
+    if (!ctx || !K || !out) return DVO_EINVAL;
+    *out = nullptr;
+    if (w < 2 || h < 2 || w >= 32768 || h >= 32768) return fail(ctx, DVO_EINVAL, "image size out of range");
+    auto u = std::make_unique<dvo_undistort>();
+    u->ctx = ctx;
+    UndistortGeom& U = u->U;
+    int rc = load_dist12(ctx, dist, ndist, U.dist);
+    if (rc) return rc;
+    U.w = w;
+    U.h = h;
+    std::memcpy(U.K, K, sizeof(U.K));
+    // cv::undistort: stripes of min(max(1, 4096 / cols), rows) rows, principal
+    // point of new_K shifted by the stripe's first row, one LU inverse each
+    U.stripe = std::min(std::max(1, (1 << 12) / w), h);
+    const int nstripes = (h + U.stripe - 1) / U.stripe;
+    std::vector<double> ir((size_t)nstripes * 9);
+    double Ar[9];
+    std::memcpy(Ar, newK ? newK : K, sizeof(Ar));
+    const double v0 = Ar[5];
+    for (int s = 0; s < nstripes; ++s) {
+        Ar[5] = v0 - (double)(s * U.stripe);
+        if (!inv3(Ar, &ir[(size_t)s * 9])) return fail(ctx, DVO_EINVAL, "new camera matrix is singular");
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    bool ok = hipMalloc(&u->d_ir, ir.size() * sizeof(double)) == hipSuccess &&
+              hipMalloc(&u->d_xy, (size_t)w * h * 2 * sizeof(int16_t)) == hipSuccess &&
+              hipMalloc(&u->d_frac, (size_t)w * h * sizeof(uint16_t)) == hipSuccess;
+    if (ok) ok = hipMemcpy(u->d_ir, ir.data(), ir.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    if (ok) ok = launch_undistort_map(U, u->d_ir, u->d_xy, u->d_frac, ctx->stream) == hipSuccess;
+    if (ok) ok = hipStreamSynchronize(ctx->stream) == hipSuccess;
+    if (!ok) {
+        hipFree(u->d_ir);
+        hipFree(u->d_xy);
+        hipFree(u->d_frac);
+        return fail(ctx, DVO_EHIP, "undistort map construction failed");
+    }
+    *out = u.release();
+    return DVO_OK;
+}
+
+void dvo_undistort_destroy(dvo_undistort* u) {
+    if (!u) return;
+    hipSetDevice(u->ctx->device);
+    hipFree(u->d_ir);
+    hipFree(u->d_xy);
+    hipFree(u->d_frac);
+    delete u;
+}
+
+int dvo_undistort_apply(dvo_undistort* u, const uint8_t* d_src, int n, int64_t src_frame_stride, int src_pitch,
+                        uint8_t* d_dst, int64_t dst_frame_stride, int dst_pitch, void* hip_stream) {
+    if (!u) return DVO_EINVAL;
+    dvo_ctx* ctx = u->ctx;
+    if (n < 0 || (n > 0 && (!d_src || !d_dst)) || src_pitch < u->U.w || dst_pitch < u->U.w)
+        return fail(ctx, DVO_EINVAL, "bad frame buffers");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    HIP_TRY(launch_undistort_remap(u->U, u->d_xy, u->d_frac, d_src, n, src_frame_stride, src_pitch, d_dst,
+                                   dst_frame_stride, dst_pitch, s));
+    return DVO_OK;
+}
+
+int dvo_undistort_get_map(dvo_undistort* u, int16_t* xy, uint16_t* frac) {
+    if (!u || !xy || !frac) return DVO_EINVAL;
+    dvo_ctx* ctx = u->ctx;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpy(xy, u->d_xy, (size_t)u->U.w * u->U.h * 2 * sizeof(int16_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(frac, u->d_frac, (size_t)u->U.w * u->U.h * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
+int dvo_undistort_image(dvo_undistort* u, const uint8_t* img, int stride, uint8_t* out, int out_stride) {
+    if (!u || !img || !out) return DVO_EINVAL;
+    dvo_ctx* ctx = u->ctx;
+    const int w = u->U.w, h = u->U.h;
+    if (stride < w || out_stride < w) return fail(ctx, DVO_EINVAL, "bad strides");
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dsrc, *ddst;
+    int rc;
+    const int pw = (w + 15) & ~15;
+    if ((rc = scratch(ctx, 24, (size_t)pw * h, &dsrc)) || (rc = scratch(ctx, 25, (size_t)pw * h, &ddst))) return rc;
+    HIP_TRY(hipMemcpy2DAsync(dsrc, pw, img, stride, w, h, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_undistort_remap(u->U, u->d_xy, u->d_frac, (const uint8_t*)dsrc, 1, 0, pw, (uint8_t*)ddst, 0, pw,
+                                   ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(out, out_stride, ddst, pw, w, h, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return DVO_OK;
+}
+
+int dvo_stream_process_undistorted(dvo_stream* s, dvo_undistort* u, const uint8_t* d_frames, int n_frames,
+                                   int64_t frame_stride, int stride, dvo_pair_record* d_records) {
+    if (!s || !u) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (u->U.w != s->cfg.width || u->U.h != s->cfg.height) return fail(ctx, DVO_EINVAL, "undistort size != stream size");
+    if (n_frames < 1 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range");
+    if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
+    if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int pw = frame_pitch(s);
+    const int64_t fs = (int64_t)pw * s->cfg.height;
+    HIP_TRY(launch_undistort_remap(u->U, u->d_xy, u->d_frac, d_frames, n_frames, frame_stride, stride, s->d_frames, fs,
+                                   pw, s->hs));
+    return run_stream(s, s->d_frames, n_frames, fs, pw, d_records, false);
+}

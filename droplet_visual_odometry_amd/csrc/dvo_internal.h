@@ -184,6 +184,18 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
                            hipEvent_t* ev = nullptr);
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
+// Undistortion (undistort.hip): camera K, distortion k1 k2 p1 p2 k3 k4 k5 k6 s1..s4.
+struct UndistortGeom {
+    int w, h, stripe;
+    double K[9];
+    double dist[12];
+};
+hipError_t launch_undistort_map(const UndistortGeom& U, const double* d_ir, int16_t* d_xy, uint16_t* d_frac,
+                                hipStream_t s);
+hipError_t launch_undistort_remap(const UndistortGeom& U, const int16_t* d_xy, const uint16_t* d_frac,
+                                  const uint8_t* d_src, int n, int64_t src_fstride, int src_pitch, uint8_t* d_dst,
+                                  int64_t dst_fstride, int dst_pitch, hipStream_t s);
+
 // carry: device [12 P_prev | 16 T_abs_prev]; updated in place.
 hipError_t launch_pose_tail(const double* Rt /*[pairs][12]*/, const int32_t* info /*[pairs][4]*/, int pairs,
                             const double* K, const double* cprev, const double* ccur, int k, double marker_length,

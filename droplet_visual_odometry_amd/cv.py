@@ -261,24 +261,55 @@ def imdecode(buf, flags=IMREAD_COLOR):
 
 
 def getOptimalNewCameraMatrix(cameraMatrix, distCoeffs, imageSize, alpha, newImgSize=None, centerPrincipalPoint=False):
-    """Zero-distortion case only: the undistorted image equals the input and the
-    camera matrix is unchanged.  Lens undistortion (remap) is SURVEY.md §8f rank 1."""
-    d = np.asarray(distCoeffs, np.float64)
-    if np.any(d != 0):
-        raise error("getOptimalNewCameraMatrix/undistort with non-zero distortion is not implemented yet "
-                    "(SURVEY.md §8f 'next'); feed undistorted mono8 frames")
+    """(newK, validPixROI) like cv2 (v3:117).  The ROI, which the reference
+    discards, is reported as the full new image."""
+    if centerPrincipalPoint:
+        raise error("centerPrincipalPoint=True is not implemented (the reference uses the default)")
     w, h = imageSize
-    return np.asarray(cameraMatrix, np.float64).copy(), (0, 0, int(w), int(h))
+    nw, nh = (w, h) if newImgSize is None or newImgSize[0] * newImgSize[1] == 0 else newImgSize
+    try:
+        K = ops.get_optimal_new_camera_matrix(cameraMatrix, distCoeffs, (w, h), alpha, (nw, nh))
+    except DVOError as e:
+        raise error(str(e)) from e
+    return K, (0, 0, int(nw), int(nh))
+
+
+class _UndistortCache:
+    """cv.undistort builds its remap table per call; the table only depends on
+    (K, dist, newK, size), so it is built once on the device and reused."""
+
+    def __init__(self):
+        self.key = None
+        self.u = None
+
+    def get(self, K, dist, newK, w, h):
+        key = (np.asarray(K, np.float64).tobytes(), np.asarray(dist, np.float64).tobytes(),
+               None if newK is None else np.asarray(newK, np.float64).tobytes(), w, h)
+        if key != self.key:
+            self.u = ops.Undistorter(K, dist, newK, w, h)
+            self.key = key
+        return self.u
+
+
+_undistort_cache = _UndistortCache()
 
 
 def undistort(src, cameraMatrix, distCoeffs, dst=None, newCameraMatrix=None):
-    d = np.asarray(distCoeffs, np.float64)
-    if np.any(d != 0):
-        raise error("undistort with non-zero distortion is not implemented yet (SURVEY.md §8f 'next')")
-    if newCameraMatrix is not None and not np.array_equal(np.asarray(newCameraMatrix, np.float64),
-                                                          np.asarray(cameraMatrix, np.float64)):
-        raise error("undistort with newCameraMatrix != cameraMatrix is not implemented yet (SURVEY.md §8f)")
-    return np.array(src, copy=True)
+    """remap(src, initUndistortRectifyMap(K, dist, I, newK), INTER_LINEAR,
+    BORDER_CONSTANT) on the GPU (v3:120)."""
+    img = np.asarray(src)
+    if img.dtype != np.uint8 or img.ndim != 2:
+        raise error("undistort is implemented for mono8 images (the reference undistorts the gray frame, v3:133-135)")
+    h, w = img.shape
+    d = np.asarray(distCoeffs if distCoeffs is not None else np.zeros(5), np.float64).ravel()
+    try:
+        out = _undistort_cache.get(cameraMatrix, d, newCameraMatrix, w, h).image(img)
+    except DVOError as e:
+        raise error(str(e)) from e
+    if dst is not None:
+        np.copyto(dst, out)
+        return dst
+    return out
 
 
 _CIRCLE3 = [(dx, dy) for dx in range(-3, 4) for dy in range(-3, 4) if round((dx * dx + dy * dy) ** 0.5) == 3]

@@ -8,6 +8,8 @@ mirrors its argument meaning, output layout and failure points:
   find_essential_mat   cv::findEssentialMat(RANSAC)       visual_odometry_v3.py:297-300
   recover_pose         cv::recoverPose                    visual_odometry_v3.py:303-306
   triangulate_points   cv::triangulatePoints              visual_odometry_v3.py:265
+  get_optimal_new_camera_matrix, Undistorter
+                       cv::getOptimalNewCameraMatrix, cv::undistort  v3:117, v3:120
 """
 from __future__ import annotations
 
@@ -15,7 +17,8 @@ import ctypes
 
 import numpy as np
 
-from ._native import (DMATCH_DTYPE, DVO_ECAP, DVO_OK, KEYPOINT_DTYPE, Context, DVOError, orb_params, ptr)
+from ._native import (DMATCH_DTYPE, DVO_ECAP, DVO_OK, KEYPOINT_DTYPE, Context, DVOError, load_library, orb_params,
+                      ptr)
 
 
 def _ctx(ctx):
@@ -140,3 +143,65 @@ def test_five_point(q1, q2, ctx=None):
     n = ctypes.c_int()
     c.check(c.lib.dvo_test_five_point(c.h, ptr(q1), ptr(q2), ptr(models), ctypes.byref(n)))
     return models[:9 * n.value].reshape(n.value, 3, 3).copy()
+
+
+# ---- image pre-processing (visual_odometry_v3.py:110-135) ----
+def get_optimal_new_camera_matrix(K, dist, size, alpha=1.0, new_size=None) -> np.ndarray:
+    """cv.getOptimalNewCameraMatrix(K, dist, size, alpha, new_size)[0] (v3:117)."""
+    lib = load_library()
+    d = np.ascontiguousarray(np.asarray(dist, np.float64).ravel())
+    w, h = size
+    nw, nh = (w, h) if new_size is None else new_size
+    out = np.zeros(9, np.float64)
+    rc = lib.dvo_get_optimal_new_camera_matrix(ptr(np.ascontiguousarray(K, np.float64).reshape(9)), ptr(d), len(d),
+                                               int(w), int(h), float(alpha), int(nw), int(nh), ptr(out))
+    if rc != DVO_OK:
+        raise DVOError(rc, "getOptimalNewCameraMatrix: bad arguments (distortion needs 0, 4, 5, 8 or 12 values)")
+    return out.reshape(3, 3)
+
+
+class Undistorter:
+    """cv.undistort(img, K, dist, None, newK) (v3:120) with the remap table built
+    once on the device.  image(): host in/out; apply(): device frames."""
+
+    def __init__(self, K, dist, newK, width: int, height: int, ctx=None):
+        self.ctx = _ctx(ctx)
+        self.w, self.h = int(width), int(height)
+        d = np.ascontiguousarray(np.asarray(dist, np.float64).ravel())
+        nk = None if newK is None else np.ascontiguousarray(newK, np.float64).reshape(9)
+        h = ctypes.c_void_p()
+        self.ctx.check(self.ctx.lib.dvo_undistort_create(self.ctx.h, ptr(np.ascontiguousarray(K, np.float64).reshape(9)),
+                                                         ptr(d), len(d), ptr(nk), self.w, self.h, ctypes.byref(h)))
+        self.h_ = h
+
+    def image(self, img: np.ndarray) -> np.ndarray:
+        img = np.ascontiguousarray(img, np.uint8)
+        if img.shape != (self.h, self.w):
+            raise DVOError(-1, f"image {img.shape} != undistorter size {(self.h, self.w)}")
+        out = np.empty_like(img)
+        self.ctx.check(self.ctx.lib.dvo_undistort_image(self.h_, ptr(img), img.strides[0], ptr(out), out.strides[0]))
+        return out
+
+    def apply(self, src, dst, hip_stream=0):
+        """Remap n device frames (uint8 torch tensors [n, H, W], rows contiguous)."""
+        n = src.shape[0]
+        self.ctx.check(self.ctx.lib.dvo_undistort_apply(self.h_, src.data_ptr(), n, src.stride(0), src.stride(1),
+                                                        dst.data_ptr(), dst.stride(0), dst.stride(1),
+                                                        ctypes.c_void_p(hip_stream) if hip_stream else None))
+
+    def map(self):
+        xy = np.zeros((self.h, self.w, 2), np.int16)
+        fr = np.zeros((self.h, self.w), np.uint16)
+        self.ctx.check(self.ctx.lib.dvo_undistort_get_map(self.h_, ptr(xy), ptr(fr)))
+        return xy, fr
+
+    def close(self):
+        if getattr(self, "h_", None):
+            self.ctx.lib.dvo_undistort_destroy(self.h_)
+            self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -47,7 +47,8 @@ class FrameStream:
     def new_records(self, n_pairs: int) -> torch.Tensor:
         return torch.zeros(max(n_pairs, 1) * PAIR_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
 
-    def process(self, frames: torch.Tensor, records: torch.Tensor | None = None, wait_torch: bool = True) -> torch.Tensor:
+    def process(self, frames: torch.Tensor, records: torch.Tensor | None = None, wait_torch: bool = True,
+                undistort=None) -> torch.Tensor:
         """Enqueue the batch on the stream's HIP stream (asynchronous).  With
         wait_torch the batch is ordered after work queued on torch's current
         stream (the frames' producer); pass False for frames already resident."""
@@ -62,6 +63,11 @@ class FrameStream:
             records = self.new_records(n - 1)
         if wait_torch:
             self._after_torch()
+        if undistort is not None:  # ops.Undistorter: frames are remapped into the stream's slab first
+            self.ctx.check(self.ctx.lib.dvo_stream_process_undistorted(
+                self.h, undistort.h_, frames.data_ptr(), n, frames.stride(0), frames.stride(1),
+                records.data_ptr() if n > 1 else None))
+            return records
         self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
                                                        frames.stride(1), records.data_ptr() if n > 1 else None))
         return records

@@ -30,6 +30,7 @@ extern "C" {
 
 typedef struct dvo_ctx dvo_ctx;
 typedef struct dvo_stream dvo_stream;
+typedef struct dvo_undistort dvo_undistort;
 
 /* cv::KeyPoint as the reference's Python sees it (28 bytes). */
 typedef struct {
@@ -95,6 +96,30 @@ int dvo_triangulate_points(dvo_ctx* ctx, const double* P1, const double* P2, con
                            int k, double* X);
 
 /* ---------------------------------------------------------------------------
+ * Image pre-processing of ros_img_msg_to_opencv_image (visual_odometry_v3.py:110-135).
+ * dist: k1 k2 p1 p2 [k3 [k4 k5 k6 [s1 s2 s3 s4]]] (ndist 0, 4, 5, 8 or 12). */
+
+/* Replaces cv::getOptimalNewCameraMatrix(K, dist, (w, h), alpha, (new_w, new_h))
+ * — visual_odometry_v3.py:117.  Host arithmetic; newK row-major 3x3. */
+int dvo_get_optimal_new_camera_matrix(const double* K, const double* dist, int ndist, int w, int h, double alpha,
+                                      int new_w, int new_h, double* newK);
+
+/* Replaces cv::undistort(img, K, dist, None, newK) — visual_odometry_v3.py:120.
+ * The remap table (OpenCV's striped initUndistortRectifyMap, CV_16SC2 + 1/32
+ * fractions) is built once on the device; apply = remap(INTER_LINEAR,
+ * BORDER_CONSTANT) of n device frames (dst may be a dvo_stream's input);
+ * hip_stream NULL = the context's stream. newK NULL = K. */
+int dvo_undistort_create(dvo_ctx* ctx, const double* K, const double* dist, int ndist, const double* newK, int w,
+                         int h, dvo_undistort** out);
+void dvo_undistort_destroy(dvo_undistort* u);
+int dvo_undistort_apply(dvo_undistort* u, const uint8_t* d_src, int n, int64_t src_frame_stride, int src_pitch,
+                        uint8_t* d_dst, int64_t dst_frame_stride, int dst_pitch, void* hip_stream);
+/* Host image in, host image out (synchronous; the drop-in's cv.undistort). */
+int dvo_undistort_image(dvo_undistort* u, const uint8_t* img, int stride, uint8_t* out, int out_stride);
+/* Test hook: the device remap table (w*h*2 int16, w*h uint16). */
+int dvo_undistort_get_map(dvo_undistort* u, int16_t* xy, uint16_t* frac);
+
+/* ---------------------------------------------------------------------------
  * Batched frame stream: the whole per-pair path of visual_odometry_calculations
  * (v3:384-408: detect both frames, match, E/RANSAC, recoverPose) for n_frames
  * device-resident frames -> n_frames-1 pair records, one launch sequence on the
@@ -129,6 +154,11 @@ void dvo_stream_destroy(dvo_stream* s);
 int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
                        dvo_pair_record* d_records);
 int dvo_stream_sync(dvo_stream* s);
+/* dvo_stream_process on undistorted frames: the n raw frames are remapped by u
+ * into the stream's own frame slab first (same HIP stream), as the reference
+ * undistorts every frame before detection (v3:120, v3:135). */
+int dvo_stream_process_undistorted(dvo_stream* s, dvo_undistort* u, const uint8_t* d_frames, int n_frames,
+                                   int64_t frame_stride, int stride, dvo_pair_record* d_records);
 /* HIP stream the batch runs on (hipStream_t as void*; each dvo_stream owns
  * one, so batches on different dvo_streams may overlap on the device). */
 void* dvo_stream_hip_stream(dvo_stream* s);

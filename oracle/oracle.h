@@ -71,6 +71,14 @@ int ora_jacobi_svd(double* At, int m, int n, int n1, double* W, double* Vt);
 int ora_solve_poly(const double* coeffs, int n, int max_iters, double* roots /*2n*/);
 int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
 
+/* Image pre-processing (undistort.cpp): cv::getOptimalNewCameraMatrix and
+ * cv::undistort (striped initUndistortRectifyMap + remap INTER_LINEAR,
+ * BORDER_CONSTANT).  xy / frac receive the 16SC2 / 16UC1 maps (w*h). */
+int ora_get_optimal_new_camera_matrix(const double* K, const double* dist, int ndist, int w, int h, double alpha,
+                                      int new_w, int new_h, double* newK);
+int ora_undistort(const uint8_t* src, int w, int h, int stride, const double* K, const double* dist, int ndist,
+                  const double* newK, uint8_t* dst, int dstride, int16_t* xy, uint16_t* frac);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,9 @@ def lib():
             "ora_jacobi_svd": [_f64p, _c, _c, _c, _f64p, _f64p],
             "ora_solve_poly": [_f64p, _c, _c, _f64p],
             "ora_ransac_update_num_iters": [_d, _d, _c, _c],
+            "ora_get_optimal_new_camera_matrix": [_f64p, _f64p, _c, _c, _c, _d, _c, _c, _f64p],
+            "ora_undistort": [_u8p, _c, _c, _c, _f64p, _f64p, _c, ctypes.c_void_p, _u8p, _c,
+                              np.ctypeslib.ndpointer(np.int16, flags="C"), np.ctypeslib.ndpointer(np.uint16, flags="C")],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -284,3 +287,30 @@ def pose_tail(K, R, t, corners_prev, corners_cur, marker_length, P_prev, T_prev)
     T_rel = _euler_matrix_sxyz(*_euler_from_matrix_rxyz(np.asarray(R, np.float64)))
     T_rel[:3, 3] = np.asarray(t, np.float64).ravel() * s
     return P_cur, T_rel, np.asarray(T_prev, np.float64).dot(T_rel)
+
+
+def get_optimal_new_camera_matrix(K, dist, w, h, alpha=1.0, new_size=None):
+    """cv.getOptimalNewCameraMatrix(K, dist, (w, h), alpha, new_size) -> newK
+    (visual_odometry_v3.py:117; restated in undistort.cpp)."""
+    d = np.ascontiguousarray(np.asarray(dist, np.float64).ravel())
+    nw, nh = (w, h) if new_size is None else new_size
+    out = np.zeros(9, np.float64)
+    lib().ora_get_optimal_new_camera_matrix(np.ascontiguousarray(K, np.float64).reshape(-1), d, len(d), w, h,
+                                            float(alpha), nw, nh, out)
+    return out.reshape(3, 3)
+
+
+def undistort(img, K, dist, newK=None):
+    """cv.undistort(img, K, dist, None, newK) (visual_odometry_v3.py:120) -> (dst, map_xy, map_frac)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    d = np.ascontiguousarray(np.asarray(dist, np.float64).ravel())
+    dst = np.zeros_like(img)
+    xy = np.zeros((h, w, 2), np.int16)
+    fr = np.zeros((h, w), np.uint16)
+    nk = None if newK is None else np.ascontiguousarray(newK, np.float64).reshape(-1)
+    rc = lib().ora_undistort(img, w, h, img.strides[0], np.ascontiguousarray(K, np.float64).reshape(-1), d, len(d),
+                             nk.ctypes.data if nk is not None else None, dst, w, xy, fr)
+    if rc:
+        raise ValueError("singular new camera matrix")
+    return dst, xy, fr

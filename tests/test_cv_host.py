@@ -47,12 +47,30 @@ def test_unsupported_modes_raise_cv_error():
         cv.triangulatePoints(None, np.zeros((3, 4)), np.zeros((2, 1)), np.zeros((2, 1)))
 
 
-def test_zero_distortion_undistort_is_identity():
-    K = np.array([[500.0, 0, 320], [0, 500, 240], [0, 0, 1]])
-    newK, roi = cv.getOptimalNewCameraMatrix(K, np.zeros((1, 5)), (640, 480), 1, (640, 480))
-    np.testing.assert_array_equal(newK, K)
-    img = np.arange(640 * 480, dtype=np.uint32).reshape(480, 640).astype(np.uint8)
-    np.testing.assert_array_equal(cv.undistort(img, K, np.zeros((1, 5)), None, newK), img)
+@pytest.mark.parametrize("dist,size", [
+    (np.zeros(5), (640, 480)),
+    (np.array([0.142541, -0.248887, -0.005254, -0.005417, 0.0]), (640, 480)),      # rosbot_calibration.yaml:22
+    (np.array([-0.296079, 0.099771, 0.000222, 0.000109, 0.0]), (1440, 1080)),      # camera_calibration.yaml:22
+    (np.array([0.1, -0.2, 0.001, -0.002, 0.05, 0.01, -0.02, 0.003]), (1280, 720)),  # rational model
+])
+def test_optimal_new_camera_matrix_matches_oracle(oracle_mod, dist, size):
+    """Host arithmetic of cv.getOptimalNewCameraMatrix(K, dist, size, 1, size)
+    (v3:117) in the library == the oracle restatement, bit for bit."""
+    K = np.array([[606.811009, 0, 325.199941], [0, 611.104701, 227.591593], [0, 0, 1.0]])
+    if size[0] > 640:
+        K = np.array([[1173.854081, 0, 747.788206], [0, 1170.565083, 574.700374], [0, 0, 1.0]])
+    got, roi = cv.getOptimalNewCameraMatrix(K, dist, size, 1, size)
+    want = oracle_mod.get_optimal_new_camera_matrix(K, dist, size[0], size[1], 1.0)
+    np.testing.assert_array_equal(got, want)
+    assert roi == (0, 0, size[0], size[1])
+    if not np.any(dist):
+        # zero distortion: K scaled by (w-1)/w, (h-1)/h (the inner rectangle is the image)
+        np.testing.assert_allclose(got[0, 0], K[0, 0] * (size[0] - 1) / size[0], rtol=1e-6)
+
+
+def test_bad_distortion_length_raises():
+    with pytest.raises(cv.error):
+        cv.getOptimalNewCameraMatrix(np.eye(3), np.zeros(3), (64, 48), 1, (64, 48))
 
 
 def test_imdecode_png_round_trip(tmp_path):
@@ -117,15 +135,12 @@ def test_dropin_non_controlled_reference_yaml(vo_module, tmp_path):
     assert (vo.frame_width, vo.frame_height) == (1400, 1080)
 
 
-def test_dropin_usb_raw_message(vo_module, tmp_path):
+def test_dropin_unknown_message_type(vo_module, tmp_path):
     y = tmp_path / "cal.yaml"
     y.write_text(CONTROLLED_YAML)
     vo = vo_module.VisualOdometry(mode="orb", calibration_file_path=str(y), controlled=True)
-    bgr = np.random.default_rng(0).integers(0, 256, (480, 640, 3), dtype=np.uint8)
-    msg = types.SimpleNamespace(data=bgr.tobytes(), height=480, width=640)
-    gray = vo.ros_img_msg_to_opencv_image(msg, "usb_raw")
-    np.testing.assert_array_equal(gray, cv.cvtColor(bgr, cv.COLOR_BGR2GRAY))
-    with pytest.raises(cv.error):
+    msg = types.SimpleNamespace(data=b"", height=480, width=640)
+    with pytest.raises(cv.error):  # image_np stays None, cvtColor asserts in the reference
         vo.ros_img_msg_to_opencv_image(msg, "unknown")
 
 

@@ -1,8 +1,9 @@
 """The drop-in VisualOdometry driven the way trajectory_evaluation_dual_process.py
 drives the reference (dual:151-166: ros_img_msg_to_opencv_image on each
-message, visual_odometry_calculations with the previous absolute pose and the
-marker corners), over a synthetic 640x480 usb_raw stream, against the oracle
-pair path + the host pose-tail restatement.  R, t, E bit-exact; the 4x4 poses
+message, i.e. BGR->gray + undistort with the optimal new camera matrix, then
+visual_odometry_calculations with the previous absolute pose and the marker
+corners), over a synthetic 640x480 usb_raw stream, against the oracle
+(undistort + pair path + the host pose-tail restatement).  R, t, E bit-exact; the 4x4 poses
 (numpy / libm on both sides, same operation order) within 1e-12."""
 import os
 import sys
@@ -38,15 +39,20 @@ def test_visual_odometry_replay(gpu_ctx, oracle_mod, tmp_path):
     msgs = [types.SimpleNamespace(data=np.repeat(f[..., None], 3, axis=2).tobytes(), height=480, width=640)
             for f in frames]
     corners = [marker_corners(i, K) for i in range(5)]
+    # the reference undistorts every frame with new_K = getOptimalNewCameraMatrix(K, 0, size, 1)
+    # (v3:117-120; zero distortion still rescales by (w-1)/w) and keeps the original K for E / pose
+    new_K = oracle_mod.get_optimal_new_camera_matrix(K, np.zeros(5), 640, 480, 1.0)
+    und = [oracle_mod.undistort(f, K, np.zeros(5), new_K)[0] for f in frames]
     T_vo = vo.robot_curr_position
     P = K @ np.hstack((np.eye(3), np.zeros((3, 1))))
     T_ref = np.eye(4)
     for i in range(1, 5):
         prev = vo.ros_img_msg_to_opencv_image(msgs[i - 1], "usb_raw")
         cur = vo.ros_img_msg_to_opencv_image(msgs[i], "usb_raw")
-        np.testing.assert_array_equal(prev, frames[i - 1])
+        np.testing.assert_array_equal(prev, und[i - 1])
+        np.testing.assert_array_equal(cur, und[i])
         T_vo, rel = vo.visual_odometry_calculations(prev, cur, T_vo, corners[i - 1], corners[i])
-        ref = oracle_mod.pair_pose(frames[i - 1], frames[i], K, 500)
+        ref = oracle_mod.pair_pose(und[i - 1], und[i], K, 500)
         np.testing.assert_array_equal(vo.essential_matrix, ref["E"])
         P, T_rel, T_ref = oracle_mod.pose_tail(K, ref["R"], ref["t_unit"], corners[i - 1], corners[i], MARKER_LEN,
                                                P, T_ref)
