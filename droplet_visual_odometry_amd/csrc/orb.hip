@@ -123,20 +123,107 @@ __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l
 
 // ------------------------------------------------------------------------
 // GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) with the 8-bit kernel
-// {18,34,49,55,49,34,18}: int row sums, (colsum + 2^15) >> 16, saturated.
-// Each thread owns 4 adjacent columns and 8 output rows of a 256 x 32 tile:
-// it walks the 14 input rows once, forms the 4 horizontal 7-tap sums of a row
-// with two v_dot4_u32_u8 per pixel on byte-aligned windows (v_alignbyte of
-// three row words), keeps a rolling 7-row window in registers and emits 4
-// pixels per row as one word.  Border columns gather bytes through reflect-101.
+// {18,34,49,55,49,34,18}: (sum over the 49 taps + 2^15) >> 16, saturated.
+// Vertical first, in packed 16-bit lanes: a column sum of 7 bytes is at most
+// 255 * 257 = 65535, so each lane keeps its 4 columns as two u16 pairs and
+// forms the vertical sums with v_pk_mad_u16 over a rolling 7-row window (one
+// word load per input row).  The horizontal taps then come from the
+// neighbouring lanes' pairs (DPP wave_shr / wave_shl) through v_dot2_u32_u16.
+// A wave covers 62 * 4 = 248 output columns (lanes 0 and 63 are the halo) and
+// kBlurR output rows; border columns gather bytes through reflect-101.
 __device__ __forceinline__ int refl101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
     return p;
 }
 
-constexpr uint32_t kGk0 = 18u | (34u << 8) | (49u << 16) | (55u << 24);
-constexpr uint32_t kGk1 = 49u | (34u << 8) | (18u << 16);
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t dpp_from_left(uint32_t v) {  // lane i <- lane i-1 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_from_right(uint32_t v) {  // lane i <- lane i+1 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
+}
+constexpr int kBlurR = kBlurTH / 4;  // output rows per wave
+
+// One wave: kBlurR output rows from row yw, columns x0 .. x0+3 per lane.
+// kInside: every lane's 4 columns lie inside the row (one word load per row);
+// otherwise each lane gathers its 4 (reflect-101) columns col[0..3] bytewise.
+// kSmall: fewer than 4 rows, rows need the general reflect-101 loop.
+template <bool kInside, bool kSmall>
+__device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int sp, uint8_t* __restrict__ dst,
+                                          int dp, int w, int h, int yw, int x0, bool store, int col_base,
+                                          uint32_t col_sel) {
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    // all input rows are loaded up front (rows past the bottom are read, reflected, but not stored)
+    uint32_t wds[kBlurR + 6];
+    // buffer loads: row offset in the scalar offset, column(s) in the vector offset
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < kBlurR + 6; ++r) {
+        const int y = yw - 3 + r;
+        const int ry = kSmall ? refl101(y, h) : min(abs(y), 2 * h - 2 - y);
+        if (kInside) {
+            wds[r] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, x0, ry * sp, 0);
+        } else {  // the lane's 4 reflected columns lie in the 8 bytes at its aligned base (span <= 6)
+            const uint32_t w0 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, col_base, ry * sp, 0);
+            const uint32_t w1 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, col_base + 4, ry * sp, 0);
+            wds[r] = __builtin_amdgcn_perm(w1, w0, col_sel);
+        }
+    }
+    u16x2 lo[7], hi[7];
+#pragma unroll
+    for (int r = 0; r < kBlurR + 6; ++r) {
+        const int y = yw - 3 + r;
+        const uint32_t wd = wds[r];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            lo[k] = lo[k + 1];
+            hi[k] = hi[k + 1];
+        }
+        lo[6] = as_u16x2(__builtin_amdgcn_perm(0u, wd, 0x0C010C00u));  // (b0, b1)
+        hi[6] = as_u16x2(__builtin_amdgcn_perm(0u, wd, 0x0C030C02u));  // (b2, b3)
+        if (r < 6) continue;
+        const u16x2 a = k18 * (lo[0] + lo[6]) + k34 * (lo[1] + lo[5]) + k49 * (lo[2] + lo[4]) + k55 * lo[3];
+        const u16x2 b = k18 * (hi[0] + hi[6]) + k34 * (hi[1] + hi[5]) + k49 * (hi[2] + hi[4]) + k55 * hi[3];
+        const uint32_t A = __builtin_bit_cast(uint32_t, a), B = __builtin_bit_cast(uint32_t, b);
+        const u16x2 al = as_u16x2(dpp_from_left(A)), bl = as_u16x2(dpp_from_left(B));
+        const u16x2 ar = as_u16x2(dpp_from_right(A)), br = as_u16x2(dpp_from_right(B));
+        constexpr uint32_t R = 1u << 15;
+        uint32_t s0 = __builtin_amdgcn_udot2(al, (u16x2){0, 18}, R, false);
+        s0 = __builtin_amdgcn_udot2(bl, (u16x2){34, 49}, s0, false);
+        s0 = __builtin_amdgcn_udot2(a, (u16x2){55, 49}, s0, false);
+        s0 = __builtin_amdgcn_udot2(b, (u16x2){34, 18}, s0, false);
+        uint32_t s1 = __builtin_amdgcn_udot2(bl, (u16x2){18, 34}, R, false);
+        s1 = __builtin_amdgcn_udot2(a, (u16x2){49, 55}, s1, false);
+        s1 = __builtin_amdgcn_udot2(b, (u16x2){49, 34}, s1, false);
+        s1 = __builtin_amdgcn_udot2(ar, (u16x2){18, 0}, s1, false);
+        uint32_t s2 = __builtin_amdgcn_udot2(bl, (u16x2){0, 18}, R, false);
+        s2 = __builtin_amdgcn_udot2(a, (u16x2){34, 49}, s2, false);
+        s2 = __builtin_amdgcn_udot2(b, (u16x2){55, 49}, s2, false);
+        s2 = __builtin_amdgcn_udot2(ar, (u16x2){34, 18}, s2, false);
+        uint32_t s3 = __builtin_amdgcn_udot2(a, (u16x2){18, 34}, R, false);
+        s3 = __builtin_amdgcn_udot2(b, (u16x2){49, 55}, s3, false);
+        s3 = __builtin_amdgcn_udot2(ar, (u16x2){49, 34}, s3, false);
+        s3 = __builtin_amdgcn_udot2(br, (u16x2){18, 0}, s3, false);
+        // byte 2 of min(s, 2^24 - 1) == min(s >> 16, 255)
+        s0 = min(s0, 0xFFFFFFu);
+        s1 = min(s1, 0xFFFFFFu);
+        s2 = min(s2, 0xFFFFFFu);
+        s3 = min(s3, 0xFFFFFFu);
+        const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0C0C0602u),
+                                                    __builtin_amdgcn_perm(s1, s0, 0x0C0C0602u), 0x05040100u);
+        if (store && y - 3 < h) {
+            uint8_t* drow = dst + (int64_t)(y - 3) * dp;
+            if (kInside || x0 + 4 <= w) {
+                *reinterpret_cast<uint32_t*>(drow + x0) = word;
+            } else {
+                for (int j = 0; j < 4 && x0 + j < w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
     const int f = blockIdx.y;
@@ -146,73 +233,34 @@ __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
     const LevelGeom& G = P.plan.L[l];
     const int t = item - G.tile_base;
     const int ty = t / G.tiles_x, tx = t - ty * G.tiles_x;
-    const int x0 = tx * kBlurTW + 4 * (threadIdx.x & 63);
-    const int y0 = ty * kBlurTH + 8 * (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = G.w, h = G.h;
-    if (x0 >= w || y0 >= h) return;
+    const int yw = ty * kBlurTH + wid * kBlurR;
+    if (yw >= h) return;
+    const int xw = tx * kBlurTW - 4;  // column of lane 0
+    const int x0 = xw + 4 * lane;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
     uint8_t* dst = blur_ptr(P, f, l);
-    const bool interior = x0 >= 4 && x0 + 8 <= w;
-    const bool rows_inside = y0 >= 3 && y0 + 10 < h;
-    uint32_t hs[7][4];
+    const bool store = lane >= 1 && lane <= 62 && x0 < w;
+    // border lanes: v_perm selector of the 4 reflect-101 columns from 2 aligned words
+    int col[4], cmin = INT_MAX;
 #pragma unroll
-    for (int r = 0; r < 14; ++r) {
-        const int yy = y0 - 3 + r;
-        const uint8_t* row = src + (int64_t)(rows_inside ? yy : refl101(yy, h)) * sp;
-        uint32_t wm, w0, w1;
-        if (interior) {
-            wm = *reinterpret_cast<const uint32_t*>(row + x0 - 4);
-            w0 = *reinterpret_cast<const uint32_t*>(row + x0);
-            w1 = *reinterpret_cast<const uint32_t*>(row + x0 + 4);
-        } else {
-            uint32_t b[3] = {0, 0, 0};
+    for (int k = 0; k < 4; ++k) {
+        col[k] = refl101(min(x0 + k, w + 2), w);  // columns past w+2 are never used: clamp
+        cmin = min(cmin, col[k]);
+    }
+    const int col_base = cmin & ~3;
+    uint32_t col_sel = 0;
 #pragma unroll
-            for (int k = 0; k < 12; ++k) b[k >> 2] |= (uint32_t)row[refl101(x0 - 4 + k, w)] << (8 * (k & 3));
-            wm = b[0];
-            w0 = b[1];
-            w1 = b[2];
-        }
-        // taps of output x0+j: bytes x0+j-3 .. x0+j+3 = window offsets j+1 .. j+7 of (wm, w0, w1)
-        uint32_t hcur[4];
-        hcur[0] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 1), kGk0,
-                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), kGk1, 0u, false),
-                                         false);
-        hcur[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 2), kGk0,
-                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), kGk1, 0u, false),
-                                         false);
-        hcur[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w0, wm, 3), kGk0,
-                                         __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), kGk1, 0u, false),
-                                         false);
-        hcur[3] = __builtin_amdgcn_udot4(w0, kGk0, __builtin_amdgcn_udot4(w1, kGk1, 0u, false), false);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) hs[k][j] = hs[k + 1][j];
-            hs[6][j] = hcur[j];
-        }
-        if (r >= 6) {
-            const int y = y0 + r - 6;
-            if (y < h) {
-                uint32_t word = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    // row sums < 2^16, weights < 2^8: 24-bit multiplies are exact
-                    const uint32_t sum = __umul24(18u, hs[0][j]) + __umul24(34u, hs[1][j]) +
-                                         __umul24(49u, hs[2][j]) + __umul24(55u, hs[3][j]) +
-                                         __umul24(49u, hs[4][j]) + __umul24(34u, hs[5][j]) +
-                                         __umul24(18u, hs[6][j]);
-                    const uint32_t v = (sum + (1u << 15)) >> 16;
-                    word |= (v > 255 ? 255u : v) << (8 * j);
-                }
-                uint8_t* drow = dst + (int64_t)y * G.bpitch;
-                if (x0 + 4 <= w) {
-                    *reinterpret_cast<uint32_t*>(drow + x0) = word;
-                } else {
-                    for (int j = 0; j < 4 && x0 + j < w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
-                }
-            }
-        }
+    for (int k = 0; k < 4; ++k) col_sel |= (uint32_t)(col[k] - col_base) << (8 * k);
+    if (h < 4) {
+        blur_wave<false, true>(src, sp, dst, G.bpitch, w, h, yw, x0, store, col_base, col_sel);
+    } else if (xw >= 0 && xw + 256 <= w) {
+        blur_wave<true, false>(src, sp, dst, G.bpitch, w, h, yw, x0, store, col_base, col_sel);
+    } else {
+        blur_wave<false, false>(src, sp, dst, G.bpitch, w, h, yw, x0, store, col_base, col_sel);
     }
 }
 
@@ -291,16 +339,29 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
     return k < 4 ? (lo >> (8 * k)) & 0xFF : (hi >> (8 * (k - 4))) & 0xFF;
 }
 
-// One FAST tile: kBandRows output rows x kFastTW output columns of one level.
-// The tile's image window (+4 rows, +7/+9 columns) is staged in LDS as words;
-// FAST scores are computed for the NMS neighbourhood (rows [r0-1, r1],
-// columns [xs-1, xe]).  Every pixel first takes the compass test (a run of 9
-// on the 16-circle covers >= 2 of the pixels 0, 4, 8, 12); survivors are
-// compacted into a per-wave ring and run the full test + score in full 64-lane
-// rounds.  Strict 3x3 NMS keeps are written per tile row in column order with
-// (offset << 16 | count) per row; select_fast_kernel restores raster order.
-constexpr int kFtLW = kFastTW + 16;  // LDS row: image columns [xs-7, xs+kFastTW+9)
-constexpr int kFtG = kFastTW / 4 + 2;  // 4-pixel groups per row, starting at LDS column 4
+// One FAST tile: kBandRows output rows x kFastTW (126) output columns of one
+// level.  The image window (rows [r0-4, r1+4), 144 columns from the aligned
+// column bx) is staged in LDS as words.  FAST scores are needed on the NMS
+// neighbourhood: score rows [r0-1, r1] x score columns [xs-1, xs+127), i.e. two
+// 64-pixel halves per score row, one pixel per lane.  Four passes, the first
+// three in full 64-lane rounds through per-wave LDS rings of pixel addresses:
+//   compass  every pixel: a run of 9 on the 16-circle contains two adjacent
+//            compass pixels (0,4 / 4,8 / 8,12 / 12,0) that are both brighter
+//            or both darker: min(max(c0,c8), max(c4,c12)) > v+t, or the dual;
+//   segment  survivors (~6%): the 16 circle compares packed into bright/dark
+//            masks with v_alignbit (sign bit shifted in), run-of-9 test;
+//   score    corners (~1%): cornerScore<16> into the LDS score plane, and the
+//            corner's address into the tile's corner list;
+//   NMS      per listed corner: strict 3x3 maximum -> keep bit of its row.
+// Keeps are written per tile row in column order with (offset << 16 | count)
+// per row; select_fast_kernel restores raster order across tiles.
+constexpr int kFtLW = 144;               // LDS row stride of the image and score planes
+constexpr int kFtRing = 128;             // per-wave ring: < 64 pending + 64 appended
+constexpr int kFtCorners = (kBandRows + 2) * 128;  // every score pixel of a tile
+__device__ __forceinline__ uint32_t lane_prefix(unsigned long long bal) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+
 __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int f = blockIdx.y;
     const int item = blockIdx.x;
@@ -313,156 +374,143 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int r0 = kBorder + b * kBandRows;
     const int r1 = min(r0 + kBandRows, h - kBorder);
     const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
-    const int bx = xs - 7;  // image column of LDS column 0 (a multiple of 4)
+    const int bx = (xs - 4) & ~3;  // image column of LDS column 0; xs - bx in [4, 7]
     const int thr = P.plan.fast_threshold;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
-    __shared__ __attribute__((aligned(16))) uint8_t img[kBandRows + 8][kFtLW];  // rows [r0-4, r1+4)
-    __shared__ __attribute__((aligned(16))) uint8_t sc[kBandRows + 2][kFtLW];   // rows [r0-1, r1+1)
-    constexpr int kRing = 512;
-    __shared__ uint32_t ring[kFastNT / 64][kRing];
-    __shared__ uint8_t kmask[kBandRows][kFtG + 2];
-    __shared__ int row_cnt[kBandRows];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ __attribute__((aligned(16))) uint8_t img[(kBandRows + 8) * kFtLW];  // rows [r0-4, r1+4)
+    __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];   // rows [r0-1, r1+1)
+    __shared__ uint16_t ring[kFastNT / 64][2][kFtRing];
+    __shared__ uint16_t corners[kFtCorners];
+    __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
+    __shared__ int ncorner;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
-    if (threadIdx.x < kBandRows) row_cnt[threadIdx.x] = 0;
+    if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+    if (threadIdx.x == 0) ncorner = 0;
     for (int i = threadIdx.x; i < (yhi - ylo) * (kFtLW / 4); i += kFastNT) {
         const int r = i / (kFtLW / 4), wd = i - r * (kFtLW / 4);
         const int col = bx + 4 * wd;
-        reinterpret_cast<uint32_t*>(img[r])[wd] =
+        reinterpret_cast<uint32_t*>(img)[i] =
             col < w ? *reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp + col) : 0u;
     }
+    for (int i = threadIdx.x; i < (kBandRows + 2) * kFtLW / 16; i += kFastNT)
+        reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    // ---- scores: rows [r0-1, r1], groups g in [1, kFtG) (image columns bx + 4g ...)
-    const unsigned long long lt = (1ull << lane) - 1;
     const int nsr = r1 - r0 + 2;
-    uint32_t* q = ring[wid];
-    int head = 0, tail = 0;  // wave-uniform
-    auto drain = [&](bool all) {
-        while (tail - head >= 64 || (all && tail > head)) {
-            const int e = head + lane;
-            if (e < tail) {
-                const uint32_t ent = q[e & (kRing - 1)];
-                const int sr = ent >> 8, lx = ent & 0xFF;
-                const uint8_t* row = &img[sr + 3][lx];
-                const int v = row[0];
-                int cc[16];
+    const int xlast = min(xe, w - 4);  // last score column (xs - 1 >= 30 >= 3 on the left)
+    const int x_lo = xs - 1 + lane;
+    const bool ok0 = x_lo <= xlast, ok1 = x_lo + 64 <= xlast;
+    uint16_t* q1 = ring[wid][0];
+    uint16_t* q2 = ring[wid][1];
+    int h1 = 0, t1 = 0, h2 = 0, t2 = 0;  // wave-uniform ring cursors
+    // score pass over q2[h2, h2 + n): scores into the plane, addresses into the corner list
+    auto score_round = [&](int n) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&ncorner, n);
+        base = __shfl(base, 0);
+        if (lane < n) {
+            const int a = q2[(h2 + lane) & (kFtRing - 1)];
+            const uint8_t* p = img + a;
+            int cc[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) cc[k] = row[kCdy[k] * kFtLW + kCdx[k]];
-                uint32_t br = 0, dk = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    br |= (uint32_t)(cc[k] > v + thr) << k;
-                    dk |= (uint32_t)(cc[k] < v - thr) << k;
-                }
-                if (has_run9(br) || has_run9(dk)) sc[sr][lx] = (uint8_t)fast_score16(cc, v, thr);
-            }
-            head += min(64, tail - head);
+            for (int k = 0; k < 16; ++k) cc[k] = p[kCdy[k] * kFtLW + kCdx[k]];
+            sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
+            corners[base + lane] = (uint16_t)(a - 3 * kFtLW);
         }
+        h2 += n;
     };
-    const int ntask = nsr * (kFtG - 1);
-    for (int t0 = wid * 64; t0 < ntask; t0 += kFastNT) {
-        const int tk = t0 + lane;
-        uint32_t cmask = 0;
-        int sr = 0, lx0 = 0;
-        if (tk < ntask) {
-            sr = tk / (kFtG - 1);
-            lx0 = 4 * (1 + tk - sr * (kFtG - 1));
-            const uint8_t* row = &img[sr + 3][0];
-            *reinterpret_cast<uint32_t*>(&sc[sr][lx0]) = 0;
-            const uint32_t up = *reinterpret_cast<const uint32_t*>(row - 3 * kFtLW + lx0);
-            const uint32_t dn = *reinterpret_cast<const uint32_t*>(row + 3 * kFtLW + lx0);
-            const uint32_t wm = *reinterpret_cast<const uint32_t*>(row + lx0 - 4);
-            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + lx0);
-            const uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + lx0 + 4);
-            const uint32_t ee = __builtin_amdgcn_alignbyte(w1, w0, 3);  // (+3, 0)
-            const uint32_t ww = __builtin_amdgcn_alignbyte(w0, wm, 1);  // (-3, 0)
+    // segment test over q1[h1, h1 + n); corners go to q2
+    auto segment_round = [&](int n) {
+        bool corner = false;
+        int a = 0;
+        if (lane < n) {
+            a = q1[(h1 + lane) & (kFtRing - 1)];
+            const uint8_t* p = img + a;
+            const int v = p[0];
+            const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
+            uint32_t br = 0, dk = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int v = (w0 >> (8 * j)) & 0xFF;
-                const int c0 = (dn >> (8 * j)) & 0xFF, c4 = (ee >> (8 * j)) & 0xFF;
-                const int c8 = (up >> (8 * j)) & 0xFF, c12 = (ww >> (8 * j)) & 0xFF;
-                const int hi = v + thr, lo = v - thr;
-                const int nb = (c0 > hi) + (c4 > hi) + (c8 > hi) + (c12 > hi);
-                const int nd = (c0 < lo) + (c4 < lo) + (c8 < lo) + (c12 < lo);
-                const int x = bx + lx0 + j;
-                if ((nb >= 2 || nd >= 2) && x >= xs - 1 && x <= xe && x >= 3 && x <= w - 4) cmask |= 1u << j;
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
+                br = __builtin_amdgcn_alignbit(br, hi - cv, 31);  // bit <- (cv > v + thr)
+                dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);  // bit <- (cv < v - thr)
             }
+            corner = has_run9(br) || has_run9(dk);
         }
-        const uint32_t ent0 = ((uint32_t)sr << 8) | (uint32_t)lx0;
+        h1 += n;
+        const unsigned long long bal = __ballot(corner);
+        if (corner) q2[(t2 + lane_prefix(bal)) & (kFtRing - 1)] = (uint16_t)a;
+        t2 += __popcll(bal);
+        if (t2 - h2 >= 64) score_round(64);
+    };
+    auto compass = [&](int a, int thr_) {
+        const int v = img[a];
+        const int c0 = img[a + 3 * kFtLW], c4 = img[a + 3], c8 = img[a - 3 * kFtLW], c12 = img[a - 3];
+        return min(max(c0, c8), max(c4, c12)) > v + thr_ || max(min(c0, c8), min(c4, c12)) < v - thr_;
+    };
+    for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
+        const int a = (sr + 3) * kFtLW + (x_lo - bx);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned long long bal = __ballot((cmask >> j) & 1);
-            if ((cmask >> j) & 1) q[(tail + __popcll(bal & lt)) & (kRing - 1)] = ent0 + j;
-            tail += __popcll(bal);
+        for (int hh = 0; hh < 2; ++hh) {
+            const bool pass = (hh ? ok1 : ok0) && compass(a + 64 * hh, thr);
+            const unsigned long long bal = __ballot(pass);
+            if (pass) q1[(t1 + lane_prefix(bal)) & (kFtRing - 1)] = (uint16_t)(a + 64 * hh);
+            t1 += __popcll(bal);
+            if (t1 - h1 >= 64) segment_round(64);
         }
-        drain(false);
     }
-    drain(true);
+    while (t1 > h1) segment_round(min(64, t1 - h1));
+    while (t2 > h2) score_round(min(64, t2 - h2));
     __syncthreads();
-    // ---- strict 3x3 NMS over rows [r0, r1), columns [xs, xe)
-    const int nrows = r1 - r0;
-    for (int tk = threadIdx.x; tk < nrows * (kFtG - 1); tk += kFastNT) {
-        const int rr = tk / (kFtG - 1), g = 1 + tk - rr * (kFtG - 1);
-        const int lx0 = 4 * g;
-        const uint8_t* s0 = &sc[rr + 1][0];
-        uint32_t m = 0;
-        const uint32_t c1 = *reinterpret_cast<const uint32_t*>(s0 + lx0);
-        if (c1) {
-            const uint32_t a0 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0 - 4),
-                           a1 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0),
-                           a2 = *reinterpret_cast<const uint32_t*>(s0 - kFtLW + lx0 + 4);
-            const uint32_t b0 = *reinterpret_cast<const uint32_t*>(s0 + lx0 - 4),
-                           b2 = *reinterpret_cast<const uint32_t*>(s0 + lx0 + 4);
-            const uint32_t d0 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0 - 4),
-                           d1 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0),
-                           d2 = *reinterpret_cast<const uint32_t*>(s0 + kFtLW + lx0 + 4);
-            const uint32_t aL = __builtin_amdgcn_alignbyte(a1, a0, 3), aR = __builtin_amdgcn_alignbyte(a2, a1, 1);
-            const uint32_t bL = __builtin_amdgcn_alignbyte(c1, b0, 3), bR = __builtin_amdgcn_alignbyte(b2, c1, 1);
-            const uint32_t dL = __builtin_amdgcn_alignbyte(d1, d0, 3), dR = __builtin_amdgcn_alignbyte(d2, d1, 1);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int sh = 8 * j;
-                const uint32_t v = (c1 >> sh) & 0xFF;
-                const uint32_t nmax =
-                    max(max(max((aL >> sh) & 0xFF, (a1 >> sh) & 0xFF), max((aR >> sh) & 0xFF, (bL >> sh) & 0xFF)),
-                        max(max((bR >> sh) & 0xFF, (dL >> sh) & 0xFF), max((d1 >> sh) & 0xFF, (dR >> sh) & 0xFF)));
-                const int x = bx + lx0 + j;
-                m |= (uint32_t)(v > nmax && x >= xs && x < xe) << j;
-            }
+    // ---- strict 3x3 NMS of the listed corners; keeps must lie in rows [r0, r1), columns [xs, xe)
+    const int nc = ncorner;
+    for (int i = threadIdx.x; i < nc; i += kFastNT) {
+        const int a = corners[i];  // score-plane address
+        const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
+        if (sr < 1 || sr > r1 - r0 || x < xs || x >= xe) continue;
+        const uint8_t* s = sc + a;
+        const uint32_t v = s[0];
+        const uint32_t nmax = max(max(max((uint32_t)s[-kFtLW - 1], (uint32_t)s[-kFtLW]),
+                                      max((uint32_t)s[-kFtLW + 1], (uint32_t)s[-1])),
+                                  max(max((uint32_t)s[1], (uint32_t)s[kFtLW - 1]),
+                                      max((uint32_t)s[kFtLW], (uint32_t)s[kFtLW + 1])));
+        if (v > nmax) {
+            const int i_col = x - (xs - 1);
+            atomicOr(&keep[sr - 1][i_col >> 5], 1u << (i_col & 31));
         }
-        kmask[rr][g] = (uint8_t)m;
-        if (m) atomicAdd(&row_cnt[rr], __popc(m));
     }
     __syncthreads();
     uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)t * G.band_cap;
     int32_t* cnt_out = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + item) * kBandRows;
+    const int nrows = r1 - r0;
     if (threadIdx.x < kBandRows) {
         int off = 0;
-        for (int rr = 0; rr < threadIdx.x; ++rr) off += row_cnt[rr];
-        cnt_out[threadIdx.x] = threadIdx.x < nrows ? (off << 16) | row_cnt[threadIdx.x] : 0;
+        for (int rr = 0; rr < threadIdx.x; ++rr)
+            off += __popc(keep[rr][0]) + __popc(keep[rr][1]) + __popc(keep[rr][2]) + __popc(keep[rr][3]);
+        const int cnt = __popc(keep[threadIdx.x][0]) + __popc(keep[threadIdx.x][1]) + __popc(keep[threadIdx.x][2]) +
+                        __popc(keep[threadIdx.x][3]);
+        cnt_out[threadIdx.x] = threadIdx.x < nrows ? (off << 16) | cnt : 0;
     }
     for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
-        if (row_cnt[rr] == 0) continue;
+        const unsigned long long k0 = (unsigned long long)keep[rr][0] | ((unsigned long long)keep[rr][1] << 32);
+        const unsigned long long k1 = (unsigned long long)keep[rr][2] | ((unsigned long long)keep[rr][3] << 32);
+        if ((k0 | k1) == 0) continue;
         int off = 0;
-        for (int k = 0; k < rr; ++k) off += row_cnt[k];
-        const int g = 1 + lane;
-        const uint32_t m = g < kFtG ? kmask[rr][g] : 0u;
-        const int cm = __popc(m);
-        int incl = cm;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y2 = __shfl_up(incl, o);
-            if (lane >= o) incl += y2;
-        }
-        int pos = off + incl - cm;
+        for (int k = 0; k < rr; ++k)
+            off += __popc(keep[k][0]) + __popc(keep[k][1]) + __popc(keep[k][2]) + __popc(keep[k][3]);
         const int y = r0 + rr;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if ((m >> j) & 1) {
-                const int lx = 4 * g + j;
-                outp[pos++] = ((uint32_t)sc[rr + 1][lx] << 24) | ((uint32_t)y << 12) | (uint32_t)(bx + lx);
-            }
+        const unsigned long long lt = (1ull << lane) - 1;
+        if ((k0 >> lane) & 1) {
+            const int x = xs - 1 + lane;
+            outp[off + __popcll(k0 & lt)] = ((uint32_t)sc[(rr + 1) * kFtLW + (x - bx)] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+        }
+        if ((k1 >> lane) & 1) {
+            const int x = xs + 63 + lane;
+            outp[off + __popcll(k0) + __popcll(k1 & lt)] =
+                ((uint32_t)sc[(rr + 1) * kFtLW + (x - bx)] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+        }
     }
 }
 
