@@ -343,23 +343,34 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 // level.  The image window (rows [r0-4, r1+4), 144 columns from the aligned
 // column bx) is staged in LDS as words.  FAST scores are needed on the NMS
 // neighbourhood: score rows [r0-1, r1] x score columns [xs-1, xs+127), i.e. two
-// 64-pixel halves per score row, one pixel per lane.  Four passes, the first
-// three in full 64-lane rounds through per-wave LDS rings of pixel addresses:
+// 64-pixel halves per score row, one pixel per lane.  Five phases separated by
+// workgroup barriers; the candidate lists are per-wave LDS segments that the
+// next phase reads as one concatenated list in full 64-lane rounds:
 //   compass  every pixel: a run of 9 on the 16-circle contains two adjacent
 //            compass pixels (0,4 / 4,8 / 8,12 / 12,0) that are both brighter
 //            or both darker: min(max(c0,c8), max(c4,c12)) > v+t, or the dual;
 //   segment  survivors (~6%): the 16 circle compares packed into bright/dark
 //            masks with v_alignbit (sign bit shifted in), run-of-9 test;
-//   score    corners (~1%): cornerScore<16> into the LDS score plane, and the
-//            corner's address into the tile's corner list;
-//   NMS      per listed corner: strict 3x3 maximum -> keep bit of its row.
-// Keeps are written per tile row in column order with (offset << 16 | count)
-// per row; select_fast_kernel restores raster order across tiles.
-constexpr int kFtLW = 144;               // LDS row stride of the image and score planes
-constexpr int kFtRing = 128;             // per-wave ring: < 64 pending + 64 appended
-constexpr int kFtCorners = (kBandRows + 2) * 128;  // every score pixel of a tile
+//   score    corners (~1%): cornerScore<16> into the LDS score plane;
+//   NMS      per corner: strict 3x3 maximum -> keep bit of its row;
+//   output   keeps per tile row in column order, (offset << 16 | count) per
+//            row; select_fast_kernel restores raster order across tiles.
+constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
+constexpr int kFtSeg = ((kBandRows + 2 + 3) / 4) * 128;  // per-wave list capacity (score rows sr == wid mod 4)
 __device__ __forceinline__ uint32_t lane_prefix(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+}
+// entry e of the concatenation of the 4 per-wave segments of `list` (counts cnt[0..3])
+__device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int e) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool past = e >= cnt[k];
+        e -= past ? cnt[k] : 0;
+        s += past ? 1 : 0;
+        if (!past) break;
+    }
+    return list[s * kFtSeg + e];
 }
 
 __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
@@ -380,94 +391,101 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int sp = level_pitch(P, l);
     __shared__ __attribute__((aligned(16))) uint8_t img[(kBandRows + 8) * kFtLW];  // rows [r0-4, r1+4)
     __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];   // rows [r0-1, r1+1)
-    __shared__ uint16_t ring[kFastNT / 64][2][kFtRing];
-    __shared__ uint16_t corners[kFtCorners];
+    __shared__ uint16_t cand[4 * kFtSeg], corner[4 * kFtSeg];
+    __shared__ int ncand[4], ncorner[4];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
-    __shared__ int ncorner;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
     if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
-    if (threadIdx.x == 0) ncorner = 0;
-    for (int i = threadIdx.x; i < (yhi - ylo) * (kFtLW / 4); i += kFastNT) {
-        const int r = i / (kFtLW / 4), wd = i - r * (kFtLW / 4);
+    {  // stage the window: 7 rows x 36 words per pass
+        constexpr int kWords = kFtLW / 4;
+        const int rr = threadIdx.x / kWords, wd = threadIdx.x - rr * kWords;
         const int col = bx + 4 * wd;
-        reinterpret_cast<uint32_t*>(img)[i] =
-            col < w ? *reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp + col) : 0u;
+        if (rr < kFastNT / kWords) {
+            for (int r = rr; r < yhi - ylo; r += kFastNT / kWords)
+                reinterpret_cast<uint32_t*>(img)[r * kWords + wd] =
+                    col < w ? *reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp + col) : 0u;
+        }
     }
     for (int i = threadIdx.x; i < (kBandRows + 2) * kFtLW / 16; i += kFastNT)
         reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
+    // ---- compass: score rows sr == wid (mod 4) into this wave's candidate segment
     const int nsr = r1 - r0 + 2;
     const int xlast = min(xe, w - 4);  // last score column (xs - 1 >= 30 >= 3 on the left)
     const int x_lo = xs - 1 + lane;
     const bool ok0 = x_lo <= xlast, ok1 = x_lo + 64 <= xlast;
-    uint16_t* q1 = ring[wid][0];
-    uint16_t* q2 = ring[wid][1];
-    int h1 = 0, t1 = 0, h2 = 0, t2 = 0;  // wave-uniform ring cursors
-    // score pass over q2[h2, h2 + n): scores into the plane, addresses into the corner list
-    auto score_round = [&](int n) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&ncorner, n);
-        base = __shfl(base, 0);
-        if (lane < n) {
-            const int a = q2[(h2 + lane) & (kFtRing - 1)];
-            const uint8_t* p = img + a;
-            int cc[16];
+    {
+        uint16_t* seg = cand + wid * kFtSeg;
+        int n = 0;  // wave-uniform
+        for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
+            const int a = (sr + 3) * kFtLW + (x_lo - bx);
 #pragma unroll
-            for (int k = 0; k < 16; ++k) cc[k] = p[kCdy[k] * kFtLW + kCdx[k]];
-            sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
-            corners[base + lane] = (uint16_t)(a - 3 * kFtLW);
-        }
-        h2 += n;
-    };
-    // segment test over q1[h1, h1 + n); corners go to q2
-    auto segment_round = [&](int n) {
-        bool corner = false;
-        int a = 0;
-        if (lane < n) {
-            a = q1[(h1 + lane) & (kFtRing - 1)];
-            const uint8_t* p = img + a;
-            const int v = p[0];
-            const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
-            uint32_t br = 0, dk = 0;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
-                br = __builtin_amdgcn_alignbit(br, hi - cv, 31);  // bit <- (cv > v + thr)
-                dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);  // bit <- (cv < v - thr)
+            for (int hh = 0; hh < 2; ++hh) {
+                const int ah = a + 64 * hh;
+                const int v = img[ah];
+                const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
+                const bool pass = (hh ? ok1 : ok0) &
+                                  ((min(max(c0, c8), max(c4, c12)) > v + thr) | (max(min(c0, c8), min(c4, c12)) < v - thr));
+                const unsigned long long bal = __ballot(pass);
+                if (pass) seg[n + lane_prefix(bal)] = (uint16_t)ah;
+                n += __popcll(bal);
             }
-            corner = has_run9(br) || has_run9(dk);
         }
-        h1 += n;
-        const unsigned long long bal = __ballot(corner);
-        if (corner) q2[(t2 + lane_prefix(bal)) & (kFtRing - 1)] = (uint16_t)a;
-        t2 += __popcll(bal);
-        if (t2 - h2 >= 64) score_round(64);
-    };
-    auto compass = [&](int a, int thr_) {
-        const int v = img[a];
-        const int c0 = img[a + 3 * kFtLW], c4 = img[a + 3], c8 = img[a - 3 * kFtLW], c12 = img[a - 3];
-        return min(max(c0, c8), max(c4, c12)) > v + thr_ || max(min(c0, c8), min(c4, c12)) < v - thr_;
-    };
-    for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
-        const int a = (sr + 3) * kFtLW + (x_lo - bx);
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const bool pass = (hh ? ok1 : ok0) && compass(a + 64 * hh, thr);
-            const unsigned long long bal = __ballot(pass);
-            if (pass) q1[(t1 + lane_prefix(bal)) & (kFtRing - 1)] = (uint16_t)(a + 64 * hh);
-            t1 += __popcll(bal);
-            if (t1 - h1 >= 64) segment_round(64);
-        }
+        if (lane == 0) ncand[wid] = n;
     }
-    while (t1 > h1) segment_round(min(64, t1 - h1));
-    while (t2 > h2) score_round(min(64, t2 - h2));
     __syncthreads();
-    // ---- strict 3x3 NMS of the listed corners; keeps must lie in rows [r0, r1), columns [xs, xe)
-    const int nc = ncorner;
-    for (int i = threadIdx.x; i < nc; i += kFastNT) {
-        const int a = corners[i];  // score-plane address
+    // ---- segment test over the concatenated candidates, corners into this wave's corner segment
+    {
+        int cnt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
+        const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+        uint16_t* seg = corner + wid * kFtSeg;
+        int n = 0;
+        for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
+            const int e = e0 + lane;
+            bool is_corner = false;
+            int a = 0;
+            if (e < total) {
+                a = seg_at(cand, cnt, e);
+                const uint8_t* p = img + a;
+                const int v = p[0];
+                const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
+                uint32_t br = 0, dk = 0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
+                    br = __builtin_amdgcn_alignbit(br, hi - cv, 31);  // bit <- (cv > v + thr)
+                    dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);  // bit <- (cv < v - thr)
+                }
+                is_corner = has_run9(br) || has_run9(dk);
+            }
+            const unsigned long long bal = __ballot(is_corner);
+            if (is_corner) seg[n + lane_prefix(bal)] = (uint16_t)a;
+            n += __popcll(bal);
+        }
+        if (lane == 0) ncorner[wid] = n;
+    }
+    __syncthreads();
+    int cnt2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cnt2[k] = ncorner[k];
+    const int ncorners = cnt2[0] + cnt2[1] + cnt2[2] + cnt2[3];
+    // ---- scores of the corners into the score plane
+    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
+        const int a = seg_at(corner, cnt2, e);
+        const uint8_t* p = img + a;
+        int cc[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cc[k] = p[kCdy[k] * kFtLW + kCdx[k]];
+        sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
+    }
+    __syncthreads();
+    // ---- strict 3x3 NMS of the corners; keeps lie in rows [r0, r1), columns [xs, xe)
+    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
+        const int a = seg_at(corner, cnt2, e) - 3 * kFtLW;  // score-plane address
         const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
         if (sr < 1 || sr > r1 - r0 || x < xs || x >= xe) continue;
         const uint8_t* s = sc + a;
@@ -482,34 +500,35 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
         }
     }
     __syncthreads();
+    // ---- output: per-row counts and offsets (a 16-lane scan in every wave), keys in column order
     uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)t * G.band_cap;
     int32_t* cnt_out = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + item) * kBandRows;
     const int nrows = r1 - r0;
-    if (threadIdx.x < kBandRows) {
-        int off = 0;
-        for (int rr = 0; rr < threadIdx.x; ++rr)
-            off += __popc(keep[rr][0]) + __popc(keep[rr][1]) + __popc(keep[rr][2]) + __popc(keep[rr][3]);
-        const int cnt = __popc(keep[threadIdx.x][0]) + __popc(keep[threadIdx.x][1]) + __popc(keep[threadIdx.x][2]) +
-                        __popc(keep[threadIdx.x][3]);
-        cnt_out[threadIdx.x] = threadIdx.x < nrows ? (off << 16) | cnt : 0;
+    int rc = 0;
+    if (lane < kBandRows && lane < nrows)
+        rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
+    int incl = rc;
+#pragma unroll
+    for (int o = 1; o < kBandRows; o <<= 1) {
+        const int y2 = __shfl_up(incl, o);
+        if (lane >= o) incl += y2;
     }
+    if (wid == 0 && lane < kBandRows) cnt_out[lane] = ((incl - rc) << 16) | rc;
+    const unsigned long long lt = (1ull << lane) - 1;
     for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
         const unsigned long long k0 = (unsigned long long)keep[rr][0] | ((unsigned long long)keep[rr][1] << 32);
         const unsigned long long k1 = (unsigned long long)keep[rr][2] | ((unsigned long long)keep[rr][3] << 32);
         if ((k0 | k1) == 0) continue;
-        int off = 0;
-        for (int k = 0; k < rr; ++k)
-            off += __popc(keep[k][0]) + __popc(keep[k][1]) + __popc(keep[k][2]) + __popc(keep[k][3]);
+        const int off = __shfl(incl, rr) - __shfl(rc, rr);
         const int y = r0 + rr;
-        const unsigned long long lt = (1ull << lane) - 1;
+        const uint8_t* srow = sc + (rr + 1) * kFtLW - bx;
         if ((k0 >> lane) & 1) {
             const int x = xs - 1 + lane;
-            outp[off + __popcll(k0 & lt)] = ((uint32_t)sc[(rr + 1) * kFtLW + (x - bx)] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+            outp[off + __popcll(k0 & lt)] = ((uint32_t)srow[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
         }
         if ((k1 >> lane) & 1) {
             const int x = xs + 63 + lane;
-            outp[off + __popcll(k0) + __popcll(k1 & lt)] =
-                ((uint32_t)sc[(rr + 1) * kFtLW + (x - bx)] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+            outp[off + __popcll(k0) + __popcll(k1 & lt)] = ((uint32_t)srow[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
         }
     }
 }
