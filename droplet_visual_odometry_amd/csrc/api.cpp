@@ -106,9 +106,10 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         if (l > 0) pyr += (int64_t)G.pitch * G.h;
         G.blur_off = blur;
         blur += (int64_t)G.bpitch * G.h;
+        // x table padded to a multiple of 4 entries at a 16-byte aligned offset (one int4 per 4 columns)
         G.xcoef_off = l == 0 ? 0 : coef;
-        G.ycoef_off = l == 0 ? 0 : coef + G.w;
-        if (l > 0) coef += G.w + G.h;
+        G.ycoef_off = l == 0 ? 0 : coef + ((G.w + 3) & ~3);
+        if (l > 0) coef += ((G.w + 3) & ~3) + ((G.h + 3) & ~3);  // y table padded the same way
         const bool usable = G.w > 2 * kBorder && G.h > 2 * kBorder;
         const int rows = usable ? G.h - 2 * kBorder : 0;
         const int wc = usable ? G.w - 2 * kBorder : 0;
@@ -140,7 +141,9 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
 
 // resize.cpp INTER_LINEAR_EXACT coefficient of destination index `val` (double
 // arithmetic as OpenCV's softdouble path; host and device agree bit for bit
-// because both are IEEE double without contraction).
+// because both are IEEE double without contraction).  Clamped positions store
+// the clamped source index with weight c1 = 0, so the kernel never branches on
+// the mode: (h0 * 256 + h1 * 0 + 2^15) >> 16 == (h0 + 128) >> 8.
 int lin_coef_packed(int val, int srcsize, int dstsize) {
     const double inv_scale = (double)dstsize / srcsize;
     const double scale = 1.0 / inv_scale;
@@ -160,8 +163,8 @@ std::vector<int32_t> resize_coefs(const Plan& p) {
     std::vector<int32_t> c(std::max(p.coef_total, 1));
     for (int l = 1; l < p.nlevels; ++l) {
         const LevelGeom &S = p.L[l - 1], &D = p.L[l];
-        for (int x = 0; x < D.w; ++x) c[D.xcoef_off + x] = lin_coef_packed(x, S.w, D.w);
-        for (int y = 0; y < D.h; ++y) c[D.ycoef_off + y] = lin_coef_packed(y, S.h, D.h);
+        for (int x = 0; x < ((D.w + 3) & ~3); ++x) c[D.xcoef_off + x] = lin_coef_packed(std::min(x, D.w - 1), S.w, D.w);
+        for (int y = 0; y < ((D.h + 3) & ~3); ++y) c[D.ycoef_off + y] = lin_coef_packed(std::min(y, D.h - 1), S.h, D.h);
     }
     return c;
 }

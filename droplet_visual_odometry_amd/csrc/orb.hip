@@ -38,86 +38,165 @@ constexpr int kCdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3}
 // Level l from level l-1: resize.cpp resize_bitExact<uchar, interpolationLinear>
 // (INTER_LINEAR_EXACT, 8-bit fixed point).  The per-column / per-row
 // coefficients are computed once per plan on the host (api.cpp resize_coefs,
-// same double arithmetic) and read from a table; each thread produces 4
-// adjacent output pixels of one row and stores them as one 32-bit word.
-__device__ __forceinline__ uint32_t hline_c(const uint8_t* row, int c, int sw) {
-    const int mode = coef_mode(c);
-    if (mode == 1) return (uint32_t)row[0] << 8;
-    if (mode == 2) return (uint32_t)row[sw - 1] << 8;
-    const int ofs = coef_ofs(c), c1 = coef_c1(c);
-    return (uint32_t)(256 - c1) * row[ofs] + (uint32_t)c1 * row[ofs + 1];
-}
+// same double arithmetic) and read from a table.  A lane produces 4 adjacent
+// output pixels (one word) on kRsR consecutive output rows of its wave: the
+// column taps come from one 16-byte table load, the row taps from scalar loads
+// (rows are wave-uniform), and all source words of the kRsR rows are issued as
+// buffer loads before any arithmetic (row offset in the scalar offset).  The
+// source bytes of 4 output columns span at most 12 bytes from an aligned base
+// (level ratio <= 1.5); wider ratios take a bytewise path.
+constexpr int kRsR = 4;
 
-// Source bytes of the 4 output columns of one thread span at most 12 bytes
-// from an aligned base (level ratio <= 1.5): up to 3 aligned word loads per
-// source row instead of 8 byte gathers, only the words actually touched.
-struct Row12 {
-    uint32_t w[3];
-    __device__ __forceinline__ uint32_t at(int i) const { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
-};
-__device__ __forceinline__ Row12 load_row12(const uint8_t* row, int base, int span_words) {
-    Row12 r;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(row + base);
-    r.w[0] = p[0];
-    r.w[1] = span_words > 1 ? p[1] : 0u;
-    r.w[2] = span_words > 2 ? p[2] : 0u;
-    return r;
-}
+__device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
 
 __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l) {
     const int f = blockIdx.z;
     const LevelGeom& S = P.plan.L[l - 1];
     const LevelGeom& D = P.plan.L[l];
-    const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x0 >= D.w || dy >= D.h) return;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x0 = blockIdx.x * 256 + 4 * lane;
+    const int dy0 = (blockIdx.y * 4 + wid) * kRsR;
+    if (dy0 >= D.h) return;
     const uint8_t* src = level_ptr(P, f, l - 1);
     const int sp = level_pitch(P, l - 1);
-    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off + (int64_t)dy * D.pitch;
-    const int cy = P.buf.coef[D.ycoef_off + dy];
-    const int ymode = coef_mode(cy);
-    const uint8_t* r0 = src + (int64_t)(ymode == 0 ? coef_ofs(cy) : (ymode == 1 ? 0 : S.h - 1)) * sp;
-    const uint8_t* r1 = r0 + sp;
-    const uint32_t cy1 = coef_c1(cy), cy0 = 256 - cy1;
-    // source taps of the 4 columns
-    int i0[4], i1[4], c1[4];
+    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
+    // taps: (source index, weight of the next index); clamped positions carry weight 0 (api.cpp)
+    const int4 cx = *reinterpret_cast<const int4*>(P.buf.coef + D.xcoef_off + min(x0, ((D.w + 3) & ~3) - 4));
+    const int4 cy = *reinterpret_cast<const int4*>(P.buf.coef + D.ycoef_off + dy0);  // wave-uniform
+    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w}, cys[4] = {cy.x, cy.y, cy.z, cy.w};
+    int i0[4], c1[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const int c = P.buf.coef[D.xcoef_off + min(x0 + j, D.w - 1)];
-        const int mode = coef_mode(c);
-        i0[j] = mode == 0 ? coef_ofs(c) : (mode == 1 ? 0 : S.w - 1);
-        i1[j] = mode == 0 ? i0[j] + 1 : i0[j];
-        c1[j] = mode == 0 ? coef_c1(c) : 0;
+        i0[j] = coef_ofs(cxs[j]);
+        c1[j] = coef_c1(cxs[j]);
     }
     const int base = i0[0] & ~3;
-    const int span_words = ((i1[3] - base) >> 2) + 1;
-    uint32_t word = 0;
-    if (span_words <= 3) {
-        const Row12 a = load_row12(r0, base, span_words);
-        Row12 b = a;
-        if (ymode == 0) b = load_row12(r1, base, span_words);
+    const bool narrow = i0[3] + 1 - base < 12;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
+    int ry0[kRsR];
+    uint32_t cy1[kRsR];
+    uint32_t wa[kRsR][3], wb[kRsR][3];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k1 = c1[j], k0 = 256 - k1;
-            const uint32_t h0 = k0 * a.at(i0[j] - base) + k1 * a.at(i1[j] - base);
-            const uint32_t h1 = k0 * b.at(i0[j] - base) + k1 * b.at(i1[j] - base);
-            const uint32_t v = ymode != 0 ? (h0 + 128) >> 8 : (h0 * cy0 + h1 * cy1 + 32768u) >> 16;
-            word |= (v > 255 ? 255u : v) << (8 * j);
-        }
-    } else {  // not reached for ORB's 1.2 pyramid; generic byte path
+    for (int rr = 0; rr < kRsR; ++rr) {
+        ry0[rr] = coef_ofs(cys[rr]);
+        cy1[rr] = coef_c1(cys[rr]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k1 = c1[j], k0 = 256 - k1;
-            const uint32_t h0 = k0 * r0[i0[j]] + k1 * r0[i1[j]];
-            const uint32_t v = ymode != 0 ? (h0 + 128) >> 8
-                                          : (h0 * cy0 + (k0 * r1[i0[j]] + k1 * r1[i1[j]]) * cy1 + 32768u) >> 16;
-            word |= (v > 255 ? 255u : v) << (8 * j);
+        for (int k = 0; k < 3; ++k) {  // row ry0 + 1 may lie past the level: weight 0, buffer reads 0
+            wa[rr][k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, base + 4 * k, ry0[rr] * sp, 0);
+            wb[rr][k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, base + 4 * k, (ry0[rr] + 1) * sp, 0);
         }
     }
-    if (x0 + 4 <= D.w) {
-        *reinterpret_cast<uint32_t*>(dst + x0) = word;
-    } else {
-        for (int j = 0; j < 4 && x0 + j < D.w; ++j) dst[x0 + j] = (uint8_t)(word >> (8 * j));
+    const bool full = x0 + 4 <= D.w;
+#pragma unroll
+    for (int rr = 0; rr < kRsR; ++rr) {
+        const int dy = dy0 + rr;
+        if (dy >= D.h) break;
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k1 = c1[j], k0 = 256 - k1;
+            uint32_t a0, a1, b0, b1;
+            if (narrow) {
+                a0 = byte_of(wa[rr], i0[j] - base);
+                a1 = byte_of(wa[rr], i0[j] + 1 - base);
+                b0 = byte_of(wb[rr], i0[j] - base);
+                b1 = byte_of(wb[rr], i0[j] + 1 - base);
+            } else {  // generic ratio: byte gathers (weight-0 taps read an in-range byte)
+                const int i1 = min(i0[j] + 1, S.w - 1), r1 = min(ry0[rr] + 1, S.h - 1);
+                a0 = src[(int64_t)ry0[rr] * sp + i0[j]];
+                a1 = src[(int64_t)ry0[rr] * sp + i1];
+                b0 = src[(int64_t)r1 * sp + i0[j]];
+                b1 = src[(int64_t)r1 * sp + i1];
+            }
+            const uint32_t h0 = k0 * a0 + k1 * a1;
+            const uint32_t h1 = k0 * b0 + k1 * b1;
+            const uint32_t v = (h0 * (256 - cy1[rr]) + h1 * cy1[rr] + 32768u) >> 16;
+            word |= (v > 255 ? 255u : v) << (8 * j);
+        }
+        uint8_t* drow = dst + (int64_t)dy * D.pitch;
+        if (full) {
+            *reinterpret_cast<uint32_t*>(drow + x0) = word;
+        } else {
+            for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+        }
+    }
+}
+
+// LDS-staged variant for level ratios <= 1.25 (ORB's 1.2 pyramid): the
+// workgroup's output tile (256 columns x 16 rows) needs at most kRsW source
+// words x kRsRows source rows; each wave stages whole source rows with
+// coalesced word loads (lane k <- word k), then every lane reads its 3 words
+// per source row from LDS.  Same arithmetic as resize_level_kernel.
+constexpr int kRsW = 96, kRsRows = 24;
+
+__global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l) {
+    __shared__ uint32_t tile[kRsRows][kRsW];
+    const int f = blockIdx.z;
+    const LevelGeom& S = P.plan.L[l - 1];
+    const LevelGeom& D = P.plan.L[l];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xa = blockIdx.x * 256;
+    const int x0 = xa + 4 * lane;
+    const int ty0 = blockIdx.y * (4 * kRsR);
+    const uint8_t* src = level_ptr(P, f, l - 1);
+    const int sp = level_pitch(P, l - 1);
+    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
+    const int32_t* cxt = P.buf.coef + D.xcoef_off;
+    const int32_t* cyt = P.buf.coef + D.ycoef_off;
+    // source window of the tile (wave-uniform)
+    const int sx0 = coef_ofs(cxt[xa]) & ~3;
+    const int nw = ((coef_ofs(cxt[min(xa + 255, D.w - 1)]) + 1 - sx0) >> 2) + 1;
+    const int sy0 = coef_ofs(cyt[ty0]);
+    const int nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
+    // this lane's taps (issued before the staging so their latency overlaps it)
+    const int4 cx = *reinterpret_cast<const int4*>(cxt + min(x0, ((D.w + 3) & ~3) - 4));
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
+    for (int r = wid; r < nr; r += 4) {
+        const int soff = (sy0 + r) * sp;
+        tile[r][lane] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane, soff, 0);
+        if (lane + 64 < nw) tile[r][lane + 64] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane + 256, soff, 0);
+    }
+    __syncthreads();
+    const int dy0 = ty0 + wid * kRsR;
+    if (dy0 >= D.h) return;
+    const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform
+    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w}, cys[4] = {cy.x, cy.y, cy.z, cy.w};
+    int i0[4], c1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        i0[j] = coef_ofs(cxs[j]) - sx0;
+        c1[j] = coef_c1(cxs[j]);
+    }
+    const int wb0 = min(i0[0] >> 2, kRsW - 3);  // lanes past the level's right edge: any in-range words
+    const int base = 4 * wb0;
+    const bool full = x0 + 4 <= D.w;
+#pragma unroll
+    for (int rr = 0; rr < kRsR; ++rr) {
+        const int dy = dy0 + rr;
+        if (dy >= D.h) break;
+        const int lr = coef_ofs(cys[rr]) - sy0;
+        const uint32_t cy1 = coef_c1(cys[rr]);
+        const int lr1 = min(lr + 1, kRsRows - 1);  // weight-0 row past the window: any in-range row
+        const uint32_t wa[3] = {tile[lr][wb0], tile[lr][wb0 + 1], tile[lr][wb0 + 2]};
+        const uint32_t wb[3] = {tile[lr1][wb0], tile[lr1][wb0 + 1], tile[lr1][wb0 + 2]};
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k1 = c1[j], k0 = 256 - k1;
+            const int o = min(i0[j] - base, 10);
+            const uint32_t h0 = k0 * byte_of(wa, o) + k1 * byte_of(wa, o + 1);
+            const uint32_t h1 = k0 * byte_of(wb, o) + k1 * byte_of(wb, o + 1);
+            const uint32_t v = (h0 * (256 - cy1) + h1 * cy1 + 32768u) >> 16;
+            word |= (v > 255 ? 255u : v) << (8 * j);
+        }
+        uint8_t* drow = dst + (int64_t)dy * D.pitch;
+        if (full) {
+            *reinterpret_cast<uint32_t*>(drow + x0) = word;
+        } else {
+            for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+        }
     }
 }
 
@@ -1019,8 +1098,14 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const int F = P.nframes;
     mark(ev, 0, 0, s);
     for (int l = 1; l < pl.nlevels; ++l) {
-        dim3 grid((pl.L[l].w + 255) / 256, (pl.L[l].h + 3) / 4, F);
-        hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
+        dim3 grid((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsR - 1) / (4 * kRsR), F);
+        // staged tile fits when both ratios are <= 1.25: 256 * 1.25 + 12 bytes <= kRsW words,
+        // 16 * 1.25 + 2 rows <= kRsRows
+        const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
+        if (lds)
+            hipLaunchKernelGGL(resize_level_lds_kernel, grid, dim3(256), 0, s, P, l);
+        else
+            hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
