@@ -1628,26 +1628,52 @@ __global__ void pose_tail_kernel(TailArgs a) {
     }
 }
 
-// Sequential prefix product T_abs[p] = T_abs[p-1] . T_rel[p] (one thread; B 4x4
-// products) and carry-out of P_prev / T_abs for the next batch.
-__global__ void pose_chain_kernel(TailArgs a) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double T[16], U[16];
-    for (int r = 0; r < 16; ++r) T[r] = a.carry[12 + r];
+// Prefix product T_abs[p] = T_abs[p-1] . T_rel[p], in pair order, and the
+// carry-out of P_prev / T_abs for the next batch.  One wave: lane 4r+c holds
+// T[r][c]; each step is U[r][c] = T[r][0]*A[0][c] + ... + T[r][3]*A[3][c] with
+// the row broadcast by DPP quad_perm, the same left-to-right arithmetic as a
+// scalar 4x4 product (bit-identical, no reassociation across steps).  T_rel is
+// staged through LDS 32 pairs at a time, off the dependency chain.
+__device__ __forceinline__ double quad_bcast(double v, int k) {
+    const int ctrl = k | (k << 2) | (k << 4) | (k << 6);
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+    switch (ctrl) {  // dpp control must be an immediate
+        case 0x00: lo = __builtin_amdgcn_mov_dpp(lo, 0x00, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x00, 0xF, 0xF, false); break;
+        case 0x55: lo = __builtin_amdgcn_mov_dpp(lo, 0x55, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x55, 0xF, 0xF, false); break;
+        case 0xAA: lo = __builtin_amdgcn_mov_dpp(lo, 0xAA, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xAA, 0xF, 0xF, false); break;
+        default: lo = __builtin_amdgcn_mov_dpp(lo, 0xFF, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xFF, 0xF, 0xF, false); break;
+    }
+    return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
+    constexpr int kChunk = 32;
+    __shared__ double tr[kChunk * 16];
+    const int lane = threadIdx.x;
     int last_ok = -1;
-    for (int p = 0; p < a.pairs; ++p) {
-        const double* Tr = a.T_rel + (int64_t)p * 16;
-        for (int r = 0; r < 4; ++r)
-            for (int c = 0; c < 4; ++c)
-                U[r * 4 + c] = T[r * 4 + 0] * Tr[0 * 4 + c] + T[r * 4 + 1] * Tr[1 * 4 + c] + T[r * 4 + 2] * Tr[2 * 4 + c] +
-                               T[r * 4 + 3] * Tr[3 * 4 + c];
-        for (int r = 0; r < 16; ++r) T[r] = U[r];
-        for (int r = 0; r < 16; ++r) a.T_abs[(int64_t)p * 16 + r] = T[r];
+    for (int p = lane; p < a.pairs; p += 64) {
         const int32_t* inf = a.info + (int64_t)p * 4;
         if (inf[3] == DVO_OK && inf[0] == 3) last_ok = p;
     }
-    if (last_ok >= 0) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
-    for (int r = 0; r < 16; ++r) a.carry[12 + r] = T[r];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
+    const int c = lane & 3;
+    double t = a.carry[12 + (lane & 15)];
+    for (int p0 = 0; p0 < a.pairs; p0 += kChunk) {
+        const int n = min(kChunk, a.pairs - p0);
+        __syncthreads();
+        for (int i = lane; i < n * 16; i += 64) tr[i] = a.T_rel[(int64_t)p0 * 16 + i];
+        __syncthreads();
+        for (int q = 0; q < n; ++q) {
+            const double* A = tr + q * 16;
+            const double a0 = A[0 * 4 + c], a1 = A[1 * 4 + c], a2 = A[2 * 4 + c], a3 = A[3 * 4 + c];
+            t = quad_bcast(t, 0) * a0 + quad_bcast(t, 1) * a1 + quad_bcast(t, 2) * a2 + quad_bcast(t, 3) * a3;
+            if (lane < 16) a.T_abs[(int64_t)(p0 + q) * 16 + lane] = t;
+        }
+    }
+    if (lane < 16) a.carry[12 + lane] = t;
+    if (lane == 0 && last_ok >= 0) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
 }
 
 __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, int mp, int mi, int32_t* out) {
