@@ -183,6 +183,105 @@ __global__ __launch_bounds__(kFNT) void nn_fused_kernel(StreamParams P) {
     }
 }
 
+// Forward + backward nearest neighbours of one stream pair on the matrix cores.
+// With descriptor bits as +-1 bytes (desc_x, written by describe_kernel), the
+// 256-term dot product s = q.t = 256 - 2 * Hamming(q, t) is an int8 GEMM:
+// v_mfma_i32_32x32x32_i8, 8 k-steps per 32x32 tile, exact in int32.  A wave
+// owns 64 queries (two 32-row strips, A fragments resident in VGPRs); the
+// workgroup streams the trains through LDS 64 at a time (16-byte chunks XOR-
+// swizzled by train so the b128 fragment reads are conflict-free).  From each
+// tile: key = (Hamming << 16) | index = (256 << 15) + index - s * 2^15, one
+// v_mad_i32_i24 per element; forward keys fold into a per-register running
+// minimum (the lane's column changes, its rows do not), backward keys fold
+// over the lane's 16 rows and into LDS / global atomicMin.  Minimum packed keys
+// give OpenCV's first-index tie rule exactly as the VALU kernels do.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+constexpr int kMWaves = 4, kMQB = 64 * kMWaves, kMStage = 64;
+constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^25), < 0x7F7F7F7F
+
+__device__ __forceinline__ int key_of(int s, int c) { return __mul24(s, -32768) + c; }
+
+__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P) {
+    __shared__ v4i bt[kMStage * 16];
+    __shared__ int colmin[kMStage];
+    const int p = blockIdx.y;
+    const int cap = P.plan.kp_cap;
+    const int nq = min(P.buf.nkp[p], cap), nt = min(P.buf.nkp[p + 1], cap);
+    const int qbase = blockIdx.x * kMQB;
+    if (qbase >= nq) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const v4i* XQ = reinterpret_cast<const v4i*>(P.buf.desc_x + (int64_t)p * cap * 256);
+    const v4i* XT = reinterpret_cast<const v4i*>(P.buf.desc_x + (int64_t)(p + 1) * cap * 256);
+    int32_t* fwd = P.buf.nn + (int64_t)p * cap;
+    int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
+    const int qs = qbase + wid * 64;  // this wave's first query
+    v4i A[2][8];
+    int best[2][16];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int q = qs + 32 * s2 + r;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) A[s2][ks] = q < nq ? XQ[(int64_t)q * 16 + 2 * ks + h] : (v4i){0, 0, 0, 0};
+#pragma unroll
+        for (int g = 0; g < 16; ++g) best[s2][g] = 0x7FFFFFFF;
+    }
+    // backward key base of register g: (256 << 15) + row(g); rows past nq never win (partial waves only)
+    const int cb0 = (256 << 15) + qs + 4 * h;
+    const bool full = qs + 64 <= nq;
+    for (int t0 = 0; t0 < nt; t0 += kMStage) {
+        __syncthreads();
+#pragma unroll
+        for (int i = threadIdx.x; i < kMStage * 16; i += 256) {
+            const int tr = i >> 4, c = i & 15, j = t0 + tr;
+            bt[tr * 16 + (c ^ (tr & 15))] = j < nt ? XT[(int64_t)j * 16 + c] : (v4i){0, 0, 0, 0};
+        }
+        if (threadIdx.x < kMStage) colmin[threadIdx.x] = 0x7FFFFFFF;
+        __syncthreads();
+#pragma unroll 1
+        for (int tt = 0; tt < kMStage / 32; ++tt) {
+            const int j = t0 + 32 * tt + r;
+            const int cf = j < nt ? (256 << 15) + j : kKeyNone;
+            v16i acc0 = {}, acc1 = {};
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const v4i B = bt[(32 * tt + r) * 16 + ((2 * ks + h) ^ (r & 15))];
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][ks], B, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1][ks], B, acc1, 0, 0, 0);
+            }
+            int cm = 0x7FFFFFFF;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int goff = (g & 3) + 8 * (g >> 2);
+                best[0][g] = min(best[0][g], key_of(acc0[g], cf));
+                best[1][g] = min(best[1][g], key_of(acc1[g], cf));
+                int k0 = key_of(acc0[g], cb0 + goff), k1 = key_of(acc1[g], cb0 + 32 + goff);
+                if (!full) {
+                    k0 = qs + 4 * h + goff < nq ? k0 : kKeyNone;
+                    k1 = qs + 32 + 4 * h + goff < nq ? k1 : kKeyNone;
+                }
+                cm = min(cm, min(k0, k1));
+            }
+            if (cm < kKeyNone && j < nt) atomicMin(&colmin[32 * tt + r], cm);
+        }
+        __syncthreads();
+        if (threadIdx.x < kMStage && t0 + threadIdx.x < nt && colmin[threadIdx.x] != 0x7FFFFFFF)
+            atomicMin(&bwd[t0 + threadIdx.x], colmin[threadIdx.x]);
+    }
+    // forward: minimum over the 32 lanes of each half (they hold the 32 columns)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            int v = best[s2][g];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) v = min(v, __shfl_xor(v, o));
+            const int qr = qs + 32 * s2 + (g & 3) + 8 * (g >> 2) + 4 * h;
+            if (r == g && qr < nq) fwd[qr] = nt > 0 ? v : -1;
+        }
+}
+
 __global__ __launch_bounds__(kNNThreads) void nn_pair_kernel(const uint8_t* q, int nq, const uint8_t* t, int nt,
                                                              int32_t* out) {
     extern __shared__ uint4 lds[];
@@ -344,7 +443,7 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     // backward keys start at 0x7F7F7F7F ("none") and are lowered by atomicMin
     hipError_t e = hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F, sizeof(int32_t) * (size_t)P.nframes * cap, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(nn_fused_kernel, dim3((cap + kFQB - 1) / kFQB, P.nframes - 1), dim3(kFNT), 0, s, P);
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3((cap + kMQB - 1) / kMQB, P.nframes - 1), dim3(256), 0, s, P);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();

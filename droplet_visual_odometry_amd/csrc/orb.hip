@@ -1066,6 +1066,12 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     unsigned long long words[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) words[q] = __ballot(t0[q] < t1[q]);
+    {  // bits 4*lane .. 4*lane+3 as +-1 bytes: (nibble * 0x204081) & 0x01010101 spreads bit j to byte j
+        const unsigned long long wq = lane < 16 ? words[0] : lane < 32 ? words[1] : lane < 48 ? words[2] : words[3];
+        const uint32_t nib = (uint32_t)(wq >> ((4 * lane) & 63)) & 0xFu;
+        const uint32_t b01 = (nib * 0x00204081u) & 0x01010101u;
+        reinterpret_cast<uint32_t*>(P.buf.desc_x + ((int64_t)f * P.plan.kp_cap + k) * 256)[lane] = ~(b01 * 0xFEu);
+    }
     if (lane == 0) {
         dvo_keypoint kp;
         kp.x = ptx;
