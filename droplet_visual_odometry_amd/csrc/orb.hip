@@ -28,7 +28,14 @@ __constant__ int8_t c_pattern[256 * 4] = {
 
 // ICAngles u_max for halfPatchSize 15 (orb.cpp computeKeyPoints): cvRound of
 // sqrt(225 - v^2) for v <= 11, then the symmetry fix-up; pinned by a test.
-__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+constexpr int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+// the same table as 16 nibbles: umax(v) = (kUmaxPacked >> 4v) & 15, no memory access
+constexpr unsigned long long umax_packed() {
+    unsigned long long p = 0;
+    for (int i = 0; i < 16; ++i) p |= (unsigned long long)c_umax[i] << (4 * i);
+    return p;
+}
+constexpr unsigned long long kUmaxPacked = umax_packed();
 
 // FAST 16-pixel Bresenham circle (dx, dy), fast.cpp makeOffsets.
 constexpr int kCdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -978,13 +985,18 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // samples are then LDS reads.
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kDPH][kDPW];
+    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kDPH + 2][kDPW];  // + 2 padding rows
     const int f = blockIdx.y;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int k = blockIdx.x * 4 + wv;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int k = blockIdx.x * 4 + wv;  // wave-uniform: keypoint fields come through scalar loads
     const int32_t* c2 = P.buf.cnt2 + f * kMaxLevels;
+    int cnt[kMaxLevels];
     int total = 0;
-    for (int l = 0; l < P.plan.nlevels; ++l) total += c2[l];
+#pragma unroll
+    for (int q = 0; q < kMaxLevels; ++q) {  // all level counts in flight at once
+        cnt[q] = q < P.plan.nlevels ? c2[q] : 0;
+        total += cnt[q];
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         P.buf.nkp[f] = total;
         if (total > P.plan.kp_cap) atomicOr(&P.buf.status[f], 1);
@@ -992,11 +1004,17 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     if (blockIdx.x * 4 >= min(total, P.plan.kp_cap)) return;  // whole block idle (uniform)
     const bool valid = k < total && k < P.plan.kp_cap;
     int l = 0, i = valid ? k : 0;
-    while (l + 1 < P.plan.nlevels && i >= c2[l]) {
-        i -= c2[l];
-        ++l;
-    }
+#pragma unroll
+    for (int q = 0; q + 1 < kMaxLevels; ++q)
+        if (l == q && q + 1 < P.plan.nlevels && i >= cnt[q]) {
+            i -= cnt[q];
+            l = q + 1;
+        }
     const LevelGeom& G = P.plan.L[l];
+    // rBRIEF pattern words of this lane's 4 bits (independent of the keypoint: issued first)
+    uint32_t pat[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const uint32_t*>(c_pattern)[q * 64 + lane];
     uint32_t key = 0;
     float response = 0.f;
     if (valid) {
@@ -1021,16 +1039,21 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         for (int it = 0; it < 16; ++it) {
             const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
             const int av = v < 0 ? -v : v;
-            const bool in = v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av];
+            const int um = (int)(kUmaxPacked >> (4 * (av > 15 ? 15 : av))) & 15;
+            const bool in = v <= 15 && (lane & 31) < 31 && au <= um;
             I[it] = in ? center[(int64_t)v * step + u] : 0;
         }
-        // ---- blurred window rows cyb-19 .. cyb+19, words from a0
-        const uint8_t* bl = blur_ptr(P, f, l);
-        const int bstep = G.bpitch;
-        for (int e = lane; e < kDPH * (kDPW / 4); e += 64) {
-            const int r = e / (kDPW / 4), wd = e - r * (kDPW / 4);
-            reinterpret_cast<uint32_t*>(patch[wv][r])[wd] =
-                *reinterpret_cast<const uint32_t*>(bl + (int64_t)(cyb - kDPR + r) * bstep + a0 + 4 * wd);
+        // ---- blurred window rows cyb-19 .. cyb+19, words from a0 (unrolled: all loads in flight)
+        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
+        constexpr int kWords = kDPH * (kDPW / 4);
+#pragma unroll
+        for (int e0 = 0; e0 < kWords; e0 += 64) {
+            // every lane loads (clamped) and stores (past the window into 2 padding rows), so no
+            // load sits behind a branch and all 7 are in flight together
+            const int e = e0 + lane, ec = min(e, kWords - 1);
+            const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
+            const uint32_t wv32 = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
+            reinterpret_cast<uint32_t*>(&patch[wv][0][0])[e] = wv32;
         }
     }
     __syncthreads();
@@ -1050,14 +1073,16 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     const float angle = fast_atan2((float)m01, (float)m10);
     // ---- rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
     const float ang = angle * (float)(M_PI / 180.f);
-    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    double sd, cd;
+    sincos((double)ang, &sd, &cd);  // == (cos(double), sin(double)): one shared range reduction
+    const float ca = (float)cd, sa = (float)sd;
     const uint8_t* pc = &patch[wv][kDPR][cxb - a0];
     int t0[4], t1[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int bit = q * 64 + lane;
-        const int px0 = c_pattern[bit * 4 + 0], py0 = c_pattern[bit * 4 + 1];
-        const int px1 = c_pattern[bit * 4 + 2], py1 = c_pattern[bit * 4 + 3];
+        const int px0 = (int8_t)(pat[q] & 0xFF), py0 = (int8_t)((pat[q] >> 8) & 0xFF);
+        const int px1 = (int8_t)((pat[q] >> 16) & 0xFF), py1 = (int8_t)(pat[q] >> 24);
         float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
         float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
         t0[q] = pc[cv_round_f(y0) * kDPW + cv_round_f(x0)];
