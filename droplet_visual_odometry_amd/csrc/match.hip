@@ -232,10 +232,18 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P) {
     const bool full = qs + 64 <= nq;
     for (int t0 = 0; t0 < nt; t0 += kMStage) {
         __syncthreads();
+        {  // 4 chunks per thread, all loads in flight (clamped index, zeroed past nt)
+            v4i v[kMStage * 16 / 256];
 #pragma unroll
-        for (int i = threadIdx.x; i < kMStage * 16; i += 256) {
-            const int tr = i >> 4, c = i & 15, j = t0 + tr;
-            bt[tr * 16 + (c ^ (tr & 15))] = j < nt ? XT[(int64_t)j * 16 + c] : (v4i){0, 0, 0, 0};
+            for (int it = 0; it < kMStage * 16 / 256; ++it) {
+                const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
+                v[it] = XT[(int64_t)min(t0 + tr, nt - 1) * 16 + c];
+            }
+#pragma unroll
+            for (int it = 0; it < kMStage * 16 / 256; ++it) {
+                const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
+                bt[tr * 16 + (c ^ (tr & 15))] = t0 + tr < nt ? v[it] : (v4i){0, 0, 0, 0};
+            }
         }
         if (threadIdx.x < kMStage) colmin[threadIdx.x] = 0x7FFFFFFF;
         __syncthreads();

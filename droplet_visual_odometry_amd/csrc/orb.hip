@@ -160,10 +160,19 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     // this lane's taps (issued before the staging so their latency overlaps it)
     const int4 cx = *reinterpret_cast<const int4*>(cxt + min(x0, ((D.w + 3) & ~3) - 4));
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
-    for (int r = wid; r < nr; r += 4) {
-        const int soff = (sy0 + r) * sp;
-        tile[r][lane] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane, soff, 0);
-        if (lane + 64 < nw) tile[r][lane + 64] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane + 256, soff, 0);
+    {  // kRsRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
+        uint32_t v0[kRsRows / 4], v1[kRsRows / 4];
+#pragma unroll
+        for (int it = 0; it < kRsRows / 4; ++it) {
+            const int soff = (sy0 + min(wid + 4 * it, nr - 1)) * sp;
+            v0[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane, soff, 0);
+            v1[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane + 256, soff, 0);
+        }
+#pragma unroll
+        for (int it = 0; it < kRsRows / 4; ++it) {
+            tile[wid + 4 * it][lane] = v0[it];
+            if (lane + 64 < kRsW) tile[wid + 4 * it][lane + 64] = v1[it];
+        }
     }
     __syncthreads();
     const int dy0 = ty0 + wid * kRsR;
@@ -442,6 +451,7 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //   output   keeps per tile row in column order, (offset << 16 | count) per
 //            row; select_fast_kernel restores raster order across tiles.
 constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
+constexpr int kFtRows = 28;                     // staged rows: kBandRows + 8, padded to 4 passes of 7
 constexpr int kFtSeg = ((kBandRows + 2 + 3) / 4) * 128;  // per-wave list capacity (score rows sr == wid mod 4)
 __device__ __forceinline__ uint32_t lane_prefix(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -475,7 +485,7 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int thr = P.plan.fast_threshold;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
-    __shared__ __attribute__((aligned(16))) uint8_t img[(kBandRows + 8) * kFtLW];  // rows [r0-4, r1+4)
+    __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];  // rows [r0-4, r1+4) + padding
     __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];   // rows [r0-1, r1+1)
     __shared__ uint16_t cand[4 * kFtSeg], corner[4 * kFtSeg];
     __shared__ int ncand[4], ncorner[4];
@@ -484,14 +494,21 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
     if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
-    {  // stage the window: 7 rows x 36 words per pass
-        constexpr int kWords = kFtLW / 4;
+    {  // stage the window: 7 rows x 36 words per pass, 4 passes, all loads in flight together.
+        // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
+        // load returns whatever lies there (or 0 past the level); rows past yhi go to padding.
+        constexpr int kWords = kFtLW / 4, kPass = kFastNT / kWords, kIters = kFtRows / kPass;
         const int rr = threadIdx.x / kWords, wd = threadIdx.x - rr * kWords;
-        const int col = bx + 4 * wd;
-        if (rr < kFastNT / kWords) {
-            for (int r = rr; r < yhi - ylo; r += kFastNT / kWords)
-                reinterpret_cast<uint32_t*>(img)[r * kWords + wd] =
-                    col < w ? *reinterpret_cast<const uint32_t*>(src + (int64_t)(ylo + r) * sp + col) : 0u;
+        if (rr < kPass) {
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
+            uint32_t v[kIters];
+#pragma unroll
+            for (int it = 0; it < kIters; ++it) {
+                const int r = min(rr + kPass * it, yhi - ylo - 1);
+                v[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + r) * sp, 0);
+            }
+#pragma unroll
+            for (int it = 0; it < kIters; ++it) reinterpret_cast<uint32_t*>(img)[(rr + kPass * it) * kWords + wd] = v[it];
         }
     }
     for (int i = threadIdx.x; i < (kBandRows + 2) * kFtLW / 16; i += kFastNT)
@@ -909,34 +926,67 @@ __global__ __launch_bounds__(kSelNT) void select_fast_kernel(StreamParams P) {
 }
 
 // orb.cpp HarrisResponses(blockSize 7, k 0.04f) on the unblurred level.
+// HarrisResponses (orb.cpp, blockSize 7, k 0.04, Sobel 3x3): 16 lanes per
+// keypoint, 4 keypoints per wave.  The keypoint's 9 x 12 byte window (rows
+// y-4..y+4, aligned columns) is fetched as 27 coalesced words into LDS, each lane
+// forms Ix, Iy at 3-4 of the 49 block positions, and the integer sums a, b, c
+// are reduced over the 16 lanes (integer: order-free), then the float response
+// is formed exactly as the scalar code does.
 __global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
+    __shared__ uint32_t win[16][32];  // one 9 x 3-word window (+ padding) per 16-lane group
     const int l = blockIdx.y, f = blockIdx.z;
     const int n = P.buf.cnt1[f * kMaxLevels + l];
     const LevelGeom& G = P.plan.L[l];
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint32_t key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
-    const int x0 = key & 0xFFF, y0 = (key >> 12) & 0xFFF;
     const uint8_t* img = level_ptr(P, f, l);
     const int step = level_pitch(P, l);
-    const uint8_t* ptr0 = img + (int64_t)(y0 - 3) * step + (x0 - 3);
-    int a = 0, b = 0, c = 0;
-    for (int yy = 0; yy < 7; ++yy) {
-        const uint8_t* r = ptr0 + (int64_t)yy * step;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, j = lane & 15;
+    uint32_t* W = win[wid * 4 + g];
+    const uint8_t* Wb = reinterpret_cast<const uint8_t*>(W);
+    const uint32_t* cand = P.buf.cand + (int64_t)f * P.plan.cand_stride + G.cand_off;
+    float* resp = P.buf.resp + (int64_t)f * P.plan.cand_stride + G.cand_off;
+    for (int base = (blockIdx.x * 4 + wid) * 4; base < n; base += gridDim.x * 16) {
+        const int i = min(base + g, n - 1);
+        const uint32_t key = cand[i];
+        const int x0 = key & 0xFFF, y0 = (key >> 12) & 0xFFF;
+        const int ax = (x0 - 4) & ~3;  // window columns ax .. ax+11 cover x0-4 .. x0+4
+        const uint8_t* wp = img + (int64_t)(y0 - 4) * step + ax;
+        const int e1 = min(j + 16, 26);
+        const uint32_t v0 = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(j / 3) * step + 4 * (j % 3));
+        const uint32_t v1 = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(e1 / 3) * step + 4 * (e1 % 3));
+        __builtin_amdgcn_wave_barrier();
+        W[j] = v0;
+        W[j + 16] = v1;  // j + 16 >= 27: padding words
+        __builtin_amdgcn_wave_barrier();
+        const int o = x0 - ax - 3;  // window column of block column 0 (pixel x0 - 3)
+        int a = 0, b = 0, c = 0;
 #pragma unroll
-        for (int xx = 0; xx < 7; ++xx) {
-            const uint8_t* p = r + xx;
-            int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
-            int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
-            a += Ix * Ix;
-            b += Iy * Iy;
-            c += Ix * Iy;
+        for (int t = 0; t < 4; ++t) {
+            const int pos = j + 16 * t;
+            if (t < 3 || pos < 49) {
+                const int py = pos / 7, px = pos - 7 * py;
+                const uint8_t* q = Wb + (1 + py) * 12 + o + px;
+                const int Ix = (q[1] - q[-1]) * 2 + (q[-12 + 1] - q[-12 - 1]) + (q[12 + 1] - q[12 - 1]);
+                const int Iy = (q[12] - q[-12]) * 2 + (q[12 - 1] - q[-12 - 1]) + (q[12 + 1] - q[-12 + 1]);
+                a += Ix * Ix;
+                b += Iy * Iy;
+                c += Ix * Iy;
+            }
         }
-    }
-    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
-    const float s4 = scale * scale * scale * scale;
-    const float fa = (float)a, fb = (float)b, fc = (float)c;
-    const float r = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
-    P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i] = r;
+#pragma unroll
+        for (int s2 = 8; s2 >= 1; s2 >>= 1) {
+            a += __shfl_xor(a, s2);
+            b += __shfl_xor(b, s2);
+            c += __shfl_xor(c, s2);
+        }
+        if (j == 0 && base + g < n) {
+            const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+            const float s4 = scale * scale * scale * scale;
+            const float fa = (float)a, fb = (float)b, fc = (float)c;
+            resp[base + g] = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1153,7 +1203,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     // only known on the device: a grid sized for 2n, grid-stride beyond that.
     int hb = 0;
     for (int l = 0; l < pl.nlevels; ++l) hb = hb > 2 * pl.L[l].nper ? hb : 2 * pl.L[l].nper;
-    hipLaunchKernelGGL(harris_kernel, dim3((hb + 255) / 256 + 1, pl.nlevels, F), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(harris_kernel, dim3((hb + 15) / 16 + 1, pl.nlevels, F), dim3(256), 0, s, P);
     hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
