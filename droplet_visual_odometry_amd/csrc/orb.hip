@@ -1034,11 +1034,17 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // blurred 39 x 44 window around it (word loads into LDS); the 512 rBRIEF
 // samples are then LDS reads.
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
+constexpr int kDKW = 1;                // keypoints per wave
+constexpr int kDKB = 4 * kDKW;         // keypoints per workgroup
+constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padding) x 9 aligned words
+
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
-    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kDPH + 2][kDPW];  // + 2 padding rows
+    __shared__ __attribute__((aligned(16))) uint8_t patch[kDKB][kDPH + 2][kDPW];  // + 2 padding rows
+    __shared__ __attribute__((aligned(16))) uint8_t icw[4][kICR][kICW];
+    __shared__ float s_ang[kDKB], s_ca[kDKB], s_sa[kDKB];
+    __shared__ int s_pc[kDKB];  // offset of the keypoint's centre in its patch
     const int f = blockIdx.y;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int k = blockIdx.x * 4 + wv;  // wave-uniform: keypoint fields come through scalar loads
     const int32_t* c2 = P.buf.cnt2 + f * kMaxLevels;
     int cnt[kMaxLevels];
     int total = 0;
@@ -1051,117 +1057,154 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         P.buf.nkp[f] = total;
         if (total > P.plan.kp_cap) atomicOr(&P.buf.status[f], 1);
     }
-    if (blockIdx.x * 4 >= min(total, P.plan.kp_cap)) return;  // whole block idle (uniform)
-    const bool valid = k < total && k < P.plan.kp_cap;
-    int l = 0, i = valid ? k : 0;
-#pragma unroll
-    for (int q = 0; q + 1 < kMaxLevels; ++q)
-        if (l == q && q + 1 < P.plan.nlevels && i >= cnt[q]) {
-            i -= cnt[q];
-            l = q + 1;
-        }
-    const LevelGeom& G = P.plan.L[l];
+    const int nk = min(total, P.plan.kp_cap);
+    if (blockIdx.x * kDKB >= nk) return;  // whole block idle (uniform)
     // rBRIEF pattern words of this lane's 4 bits (independent of the keypoint: issued first)
     uint32_t pat[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const uint32_t*>(c_pattern)[q * 64 + lane];
-    uint32_t key = 0;
-    float response = 0.f;
-    if (valid) {
-        key = P.buf.cand[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
-        response = P.buf.resp[(int64_t)f * P.plan.cand_stride + G.cand_off + i];
-    }
-    const int kx = key & 0xFFF, ky = (key >> 12) & 0xFFF;
-    const float scale = G.scale;
-    const float ptx = (float)kx * scale, pty = (float)ky * scale;
-    const float sc = 1.f / scale;
-    const int cxb = cv_round_f(ptx * sc), cyb = cv_round_f(pty * sc);  // orb.cpp: center = &img(cvRound(pt*sc))
+    // ICAngles disk membership of this lane's 16 samples (u = column, v = row): keypoint independent
     const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
     const int au = u < 0 ? -u : u;
-    int I[16];
-    const int a0 = (cxb - kDPR) & ~3;
-    if (valid) {
-        // ---- ICAngles rows (unblurred level), all 16 loads in flight
-        const uint8_t* img = level_ptr(P, f, l);
-        const int step = level_pitch(P, l);
-        const uint8_t* center = img + (int64_t)ky * step + kx;
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
-            const int av = v < 0 ? -v : v;
-            const int um = (int)(kUmaxPacked >> (4 * (av > 15 ? 15 : av))) & 15;
-            const bool in = v <= 15 && (lane & 31) < 31 && au <= um;
-            I[it] = in ? center[(int64_t)v * step + u] : 0;
-        }
-        // ---- blurred window rows cyb-19 .. cyb+19, words from a0 (unrolled: all loads in flight)
-        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
-        constexpr int kWords = kDPH * (kDPW / 4);
-#pragma unroll
-        for (int e0 = 0; e0 < kWords; e0 += 64) {
-            // every lane loads (clamped) and stores (past the window into 2 padding rows), so no
-            // load sits behind a branch and all 7 are in flight together
-            const int e = e0 + lane, ec = min(e, kWords - 1);
-            const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
-            const uint32_t wv32 = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
-            reinterpret_cast<uint32_t*>(&patch[wv][0][0])[e] = wv32;
-        }
-    }
-    __syncthreads();
-    if (!valid) return;
-    int m01 = 0, m10 = 0;
+    uint32_t inbits = 0;
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
-        const int v = 2 * it + (lane >> 5) - 15;
-        m10 += u * I[it];
-        m01 += v * I[it];
+        const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
+        const int av = v < 0 ? -v : v;
+        const int um = (int)(kUmaxPacked >> (4 * (av > 15 ? 15 : av))) & 15;
+        inbits |= (uint32_t)(v <= 15 && (lane & 31) < 31 && au <= um) << it;
     }
+    // keypoint (level, index, key) of this wave's 4 slots, keys requested together
+    int lv[kDKW], ix[kDKW];
+    uint32_t keys[kDKW];
+    float resps[kDKW];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o);
-        m01 += __shfl_xor(m01, o);
-    }
-    const float angle = fast_atan2((float)m01, (float)m10);
-    // ---- rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
-    const float ang = angle * (float)(M_PI / 180.f);
-    double sd, cd;
-    sincos((double)ang, &sd, &cd);  // == (cos(double), sin(double)): one shared range reduction
-    const float ca = (float)cd, sa = (float)sd;
-    const uint8_t* pc = &patch[wv][kDPR][cxb - a0];
-    int t0[4], t1[4];
+    for (int kk = 0; kk < kDKW; ++kk) {
+        int l = 0, i = min(blockIdx.x * kDKB + wv * kDKW + kk, nk - 1);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int bit = q * 64 + lane;
-        const int px0 = (int8_t)(pat[q] & 0xFF), py0 = (int8_t)((pat[q] >> 8) & 0xFF);
-        const int px1 = (int8_t)((pat[q] >> 16) & 0xFF), py1 = (int8_t)(pat[q] >> 24);
-        float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
-        float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
-        t0[q] = pc[cv_round_f(y0) * kDPW + cv_round_f(x0)];
-        t1[q] = pc[cv_round_f(y1) * kDPW + cv_round_f(x1)];
+        for (int q = 0; q + 1 < kMaxLevels; ++q)
+            if (l == q && q + 1 < P.plan.nlevels && i >= cnt[q]) {
+                i -= cnt[q];
+                l = q + 1;
+            }
+        lv[kk] = l;
+        ix[kk] = i;
+        keys[kk] = P.buf.cand[(int64_t)f * P.plan.cand_stride + P.plan.L[l].cand_off + i];
+        resps[kk] = P.buf.resp[(int64_t)f * P.plan.cand_stride + P.plan.L[l].cand_off + i];
     }
-    unsigned long long words[4];
+    // ---- phase 1: per keypoint of this wave, fetch both windows, IC angle
+    for (int kk = 0; kk < kDKW; ++kk) {
+        const int slot = wv * kDKW + kk;
+        const int k = blockIdx.x * kDKB + slot;
+        if (k >= nk) break;  // wave-uniform
+        const int l = lv[kk];
+        const LevelGeom& G = P.plan.L[l];
+        const uint32_t key = keys[kk];
+        const int kx = key & 0xFFF, ky = (key >> 12) & 0xFFF;
+        const float scale = G.scale;
+        const float ptx = (float)kx * scale, pty = (float)ky * scale;
+        const float sc = 1.f / scale;
+        const int cxb = cv_round_f(ptx * sc), cyb = cv_round_f(pty * sc);  // orb.cpp: center = &img(cvRound(pt*sc))
+        const int a0 = (cxb - kDPR) & ~3;
+        const int ai = (kx - 15) & ~3;
+        {  // all 5 IC-window and 7 patch word loads in flight (clamped loads, padded stores)
+            const uint8_t* img = level_ptr(P, f, l) + (int64_t)(ky - 15) * level_pitch(P, l) + ai;
+            const int step = level_pitch(P, l);
+            const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
+            constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
+            uint32_t iv[5], pv[7];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) words[q] = __ballot(t0[q] < t1[q]);
-    {  // bits 4*lane .. 4*lane+3 as +-1 bytes: (nibble * 0x204081) & 0x01010101 spreads bit j to byte j
-        const unsigned long long wq = lane < 16 ? words[0] : lane < 32 ? words[1] : lane < 48 ? words[2] : words[3];
-        const uint32_t nib = (uint32_t)(wq >> ((4 * lane) & 63)) & 0xFu;
-        const uint32_t b01 = (nib * 0x00204081u) & 0x01010101u;
-        reinterpret_cast<uint32_t*>(P.buf.desc_x + ((int64_t)f * P.plan.kp_cap + k) * 256)[lane] = ~(b01 * 0xFEu);
+            for (int t = 0; t < 5; ++t) {
+                const int ec = min(64 * t + lane, kIW - 1);
+                const int rc = ec / (kICW / 4), wc = ec - rc * (kICW / 4);
+                iv[t] = *reinterpret_cast<const uint32_t*>(img + (int64_t)rc * step + 4 * wc);
+            }
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                const int ec = min(64 * t + lane, kPW - 1);
+                const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
+                pv[t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = iv[t];
+#pragma unroll
+            for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pv[t];
+            __builtin_amdgcn_wave_barrier();
+        }
+        // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
+        const uint8_t* col = &icw[wv][0][0] + (kx - ai) + u;
+        int sI = 0, m01 = 0;
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int v = 2 * it + (lane >> 5) - 15;
+            const int I = (inbits >> it) & 1 ? (int)col[(v + 15) * kICW] : 0;
+            sI += I;
+            m01 += v * I;
+        }
+        int m10 = u * sI;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m10 += __shfl_xor(m10, o);
+            m01 += __shfl_xor(m01, o);
+        }
+        if (lane == 0) {
+            const float angle = fast_atan2((float)m01, (float)m10);
+            s_ang[slot] = angle;
+            s_pc[slot] = kDPR * kDPW + (cxb - a0);
+            dvo_keypoint kp;
+            kp.x = ptx;
+            kp.y = pty;
+            kp.size = 31 * scale;
+            kp.angle = angle;
+            kp.response = resps[kk];
+            kp.octave = l;
+            kp.class_id = -1;
+            P.buf.kps[(int64_t)f * P.plan.kp_cap + k] = kp;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0) {
-        dvo_keypoint kp;
-        kp.x = ptx;
-        kp.y = pty;
-        kp.size = 31 * scale;
-        kp.angle = angle;
-        kp.response = response;
-        kp.octave = l;
-        kp.class_id = -1;
-        P.buf.kps[(int64_t)f * P.plan.kp_cap + k] = kp;
-        unsigned long long* d = reinterpret_cast<unsigned long long*>(P.buf.desc + ((int64_t)f * P.plan.kp_cap + k) * 32);
-        d[0] = words[0];
-        d[1] = words[1];
-        d[2] = words[2];
-        d[3] = words[3];
+    __syncthreads();
+    // ---- phase 2: the workgroup's 16 rotations in one evaluation (orb.cpp: (float)cos / sin of
+    // angle * (float)(CV_PI / 180))
+    if (threadIdx.x < kDKB) {
+        const float ang = s_ang[threadIdx.x] * (float)(M_PI / 180.f);
+        double sd, cd;
+        sincos((double)ang, &sd, &cd);
+        s_ca[threadIdx.x] = (float)cd;
+        s_sa[threadIdx.x] = (float)sd;
+    }
+    __syncthreads();
+    // ---- phase 3: rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
+    for (int kk = 0; kk < kDKW; ++kk) {
+        const int slot = wv * kDKW + kk;
+        const int k = blockIdx.x * kDKB + slot;
+        if (k >= nk) break;
+        const float ca = s_ca[slot], sa = s_sa[slot];
+        const uint8_t* pc = &patch[slot][0][0] + s_pc[slot];
+        int t0[4], t1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int px0 = (int8_t)(pat[q] & 0xFF), py0 = (int8_t)((pat[q] >> 8) & 0xFF);
+            const int px1 = (int8_t)((pat[q] >> 16) & 0xFF), py1 = (int8_t)(pat[q] >> 24);
+            float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
+            float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
+            t0[q] = pc[cv_round_f(y0) * kDPW + cv_round_f(x0)];
+            t1[q] = pc[cv_round_f(y1) * kDPW + cv_round_f(x1)];
+        }
+        unsigned long long words[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) words[q] = __ballot(t0[q] < t1[q]);
+        {  // bits 4*lane .. 4*lane+3 as +-1 bytes: (nibble * 0x204081) & 0x01010101 spreads bit j to byte j
+            const unsigned long long wq = lane < 16 ? words[0] : lane < 32 ? words[1] : lane < 48 ? words[2] : words[3];
+            const uint32_t nib = (uint32_t)(wq >> ((4 * lane) & 63)) & 0xFu;
+            const uint32_t b01 = (nib * 0x00204081u) & 0x01010101u;
+            reinterpret_cast<uint32_t*>(P.buf.desc_x + ((int64_t)f * P.plan.kp_cap + k) * 256)[lane] = ~(b01 * 0xFEu);
+        }
+        if (lane < 4) {
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(P.buf.desc + ((int64_t)f * P.plan.kp_cap + k) * 32);
+            d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        }
     }
 }
 
@@ -1207,7 +1250,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
-    hipLaunchKernelGGL(describe_kernel, dim3((pl.kp_cap + 3) / 4, F), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(describe_kernel, dim3((pl.kp_cap + kDKB - 1) / kDKB, F), dim3(256), 0, s, P);
     mark(ev, 4, 1, s);
     return hipGetLastError();
 }
