@@ -490,6 +490,7 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
     __shared__ uint16_t cand[4 * kFtSeg], corner[4 * kFtSeg];
     __shared__ int ncand[4], ncorner[4];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
+    __shared__ int row_off[kBandRows];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int ylo = r0 - 4, yhi = min(r1 + 4, h);
@@ -603,36 +604,36 @@ __global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
         }
     }
     __syncthreads();
-    // ---- output: per-row counts and offsets (a 16-lane scan in every wave), keys in column order
+    // ---- output: row counts and offsets (one 16-lane scan), then every kept corner writes its key
+    // at row offset + kept columns before it: keys of a row land in column order
     uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)t * G.band_cap;
-    int32_t* cnt_out = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + item) * kBandRows;
     const int nrows = r1 - r0;
-    int rc = 0;
-    if (lane < kBandRows && lane < nrows)
-        rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
-    int incl = rc;
+    if (wid == 0) {
+        int rc = 0;
+        if (lane < kBandRows && lane < nrows)
+            rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
+        int incl = rc;
 #pragma unroll
-    for (int o = 1; o < kBandRows; o <<= 1) {
-        const int y2 = __shfl_up(incl, o);
-        if (lane >= o) incl += y2;
+        for (int o = 1; o < kBandRows; o <<= 1) {
+            const int y2 = __shfl_up(incl, o);
+            if (lane >= o) incl += y2;
+        }
+        if (lane < kBandRows) {
+            row_off[lane] = incl - rc;
+            P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = ((incl - rc) << 16) | rc;
+        }
     }
-    if (wid == 0 && lane < kBandRows) cnt_out[lane] = ((incl - rc) << 16) | rc;
-    const unsigned long long lt = (1ull << lane) - 1;
-    for (int rr = wid; rr < nrows; rr += kFastNT / 64) {
-        const unsigned long long k0 = (unsigned long long)keep[rr][0] | ((unsigned long long)keep[rr][1] << 32);
-        const unsigned long long k1 = (unsigned long long)keep[rr][2] | ((unsigned long long)keep[rr][3] << 32);
-        if ((k0 | k1) == 0) continue;
-        const int off = __shfl(incl, rr) - __shfl(rc, rr);
-        const int y = r0 + rr;
-        const uint8_t* srow = sc + (rr + 1) * kFtLW - bx;
-        if ((k0 >> lane) & 1) {
-            const int x = xs - 1 + lane;
-            outp[off + __popcll(k0 & lt)] = ((uint32_t)srow[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
-        }
-        if ((k1 >> lane) & 1) {
-            const int x = xs + 63 + lane;
-            outp[off + __popcll(k0) + __popcll(k1 & lt)] = ((uint32_t)srow[x] << 24) | ((uint32_t)y << 12) | (uint32_t)x;
-        }
+    __syncthreads();
+    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
+        const int a = seg_at(corner, cnt2, e) - 3 * kFtLW;
+        const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
+        if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
+        const int i_col = x - (xs - 1), w = i_col >> 5;
+        const uint32_t* kr = keep[sr - 1];
+        if (!((kr[w] >> (i_col & 31)) & 1)) continue;
+        int before = __popc(kr[w] & ((1u << (i_col & 31)) - 1));
+        for (int q = 0; q < w; ++q) before += __popc(kr[q]);
+        outp[row_off[sr - 1] + before] = ((uint32_t)sc[a] << 24) | ((uint32_t)(r0 + sr - 1) << 12) | (uint32_t)x;
     }
 }
 
