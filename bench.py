@@ -191,7 +191,7 @@ def main():
         per_call = {k: v / calls for k, v in stage_ms.items()}
         # roofline of the dominant single-kernel stage (one launch per step, so the
         # HIP-event time on the library's stream is that kernel's duration)
-        single = {"fast": "fast_band_kernel", "blur": "blur_kernel", "describe": "describe_kernel"}
+        single = {"fast": "fast_strip_kernel", "blur": "blur_kernel", "describe": "describe_kernel"}
         dom = max(single, key=lambda k: per_call.get(k, 0.0))
         bytes_per_launch = sb[dom] * (B + 1)
         achieved = bytes_per_launch / (per_call[dom] * 1e-3) / 1e9

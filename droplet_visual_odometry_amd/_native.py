@@ -19,7 +19,8 @@ except Exception:  # pragma: no cover - torch is always present in this image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdvo_hip.so")
+# DVO_LIB_PATH: an experiment build of the same sources (tools/ A/B runs); default the in-tree product build
+LIB_PATH = os.environ.get("DVO_LIB_PATH") or os.path.join(HERE, "lib", "libdvo_hip.so")
 
 DVO_OK = 0
 DVO_EINVAL = -1

@@ -46,28 +46,33 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _stale(objs):
-    if not os.path.exists(LIB):
+def _stale(objs, lib=LIB):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
         os.path.join(HERE, "..", "include", "dvo.h"), os.path.join(HERE, "..", "data", "orb_bit_pattern_31.inc"),
         __file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
+    """Compile and link libdvo_hip.so.  `out`/`defines` build an experiment
+    variant beside it (tools/: A/B timing through DVO_LIB_PATH); the product
+    library is always the default build."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    LIB = out
+    objdir = os.path.join(os.path.dirname(out), "obj" if out == globals()["LIB"] else "obj_" + os.path.basename(out))
+    os.makedirs(objdir, exist_ok=True)
     srcs = sources()
-    objs = [os.path.join(LIBDIR, "obj", os.path.basename(s) + ".o") for s in srcs]
-    if not force and not _stale(objs):
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+    if not force and not _stale(objs, LIB):
         return LIB
 
     def compile_one(pair):
         src, obj = pair
         lang = ["-x", "hip"]
-        cmd = [hipcc, *lang, *CXXFLAGS, "-c", src, "-o", obj]
+        cmd = [hipcc, *lang, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -92,7 +92,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     int nper[kMaxLevels];
     features_per_level(nfeatures, kMaxLevels, nper);
     int64_t pyr = 0, blur = 0, bcand = 0, cand = 0;
-    int bands = 0, tiles = 0, coef = 0;
+    int bands = 0, strips = 0, tiles = 0, coef = 0;
     for (int l = 0; l < kMaxLevels; ++l) {
         LevelGeom& G = p.L[l];
         G.scale = (float)std::pow((double)1.2f, (double)l);  // getScale
@@ -117,6 +117,8 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         G.ntx = (wc + kFastTW - 1) / kFastTW;
         G.band_base = bands;
         bands += G.nbands * G.ntx;
+        G.strip_base = strips;
+        strips += G.nbands > 0 ? G.ntx : 0;
         G.band_cap = (kBandRows / 2) * (kFastTW / 2) + 4;  // strict NMS: <= 1 keep per 2x2
         G.band_cand_off = bcand;
         bcand += (int64_t)G.nbands * G.ntx * G.band_cap;
@@ -131,6 +133,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     p.pyr_stride = (pyr + 255) & ~(int64_t)255;
     p.blur_stride = (blur + 255) & ~(int64_t)255;
     p.total_bands = bands;
+    p.total_strips = strips;
     p.band_cand_stride = (bcand + 63) & ~(int64_t)63;
     p.cand_stride = (cand + 63) & ~(int64_t)63;
     p.total_tiles = tiles;

@@ -34,6 +34,7 @@ struct LevelGeom {
     int nbands;           // FAST tile rows (kBandRows each) over rows [31, h-31)
     int ntx;              // FAST tile columns (kFastTW each) over columns [31, w-31)
     int band_base;        // first FAST tile of this level within a frame (tile = band * ntx + col)
+    int strip_base;       // first FAST column strip of this level within a frame (strip = level's col)
     int band_cap;         // candidate capacity per FAST tile
     int64_t band_cand_off;// u32 offset of this level's first tile slot within a frame
     int cand_cap;         // candidate capacity of the level (>= sum of its band caps)
@@ -48,6 +49,7 @@ struct Plan {
     int64_t pyr_stride;       // bytes per frame (levels 1..7)
     int64_t blur_stride;      // bytes per frame (levels 0..7)
     int total_bands;          // FAST tiles per frame
+    int total_strips;         // FAST column strips per frame (one workgroup each)
     int64_t band_cand_stride; // u32 per frame
     int64_t cand_stride;      // u32 per frame
     int total_tiles;          // blur tiles per frame

@@ -7,8 +7,8 @@
 // Stages (DESIGN.md §4 lists the roofline of each):
 //   resize_level_kernel   INTER_LINEAR_EXACT 8-bit fixed point, level l-1 -> l
 //   blur_kernel           GaussianBlur 7x7 sigma 2, 8-bit fixed-point separable
-//   fast_band_kernel      FAST-9/16 + strict 3x3 NMS + border cut + raster-ordered
-//                         compaction, one 8-row band of one level per workgroup
+//   fast_strip_kernel     FAST-9/16 + strict 3x3 NMS + border cut + per-row
+//                         compaction, one column strip of one level per workgroup
 //   select_fast_kernel    KeyPointsFilter::retainBest(2n) by FAST score: exact
 //                         emulation of libstdc++ nth_element + partition
 //   harris_kernel         HarrisResponses(blockSize 7, k 0.04)
@@ -434,13 +434,19 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
     return k < 4 ? (lo >> (8 * k)) & 0xFF : (hi >> (8 * (k - 4))) & 0xFF;
 }
 
-// One FAST tile: kBandRows output rows x kFastTW (126) output columns of one
-// level.  The image window (rows [r0-4, r1+4), 144 columns from the aligned
-// column bx) is staged in LDS as words.  FAST scores are needed on the NMS
-// neighbourhood: score rows [r0-1, r1] x score columns [xs-1, xs+127), i.e. two
-// 64-pixel halves per score row, one pixel per lane.  Five phases separated by
-// workgroup barriers; the candidate lists are per-wave LDS segments that the
-// next phase reads as one concatenated list in full 64-lane rounds:
+// FAST over one column strip of one level.  The workgroup walks the strip's
+// tiles (kBandRows output rows x kFastTW (126) output columns) top to bottom.
+// The image window of a tile (rows [r0-4, r0+20), 144 columns from the aligned
+// column bx) lives in LDS as words; the next tile's 16 new rows are loaded into
+// registers while the current tile is processed (the load latency hides behind
+// the compute), and its last 8 rows are carried to the top of the window, so
+// every image byte is fetched from HBM once.  FAST scores are needed on the
+// NMS neighbourhood, score rows [r0-1, r1] x score columns [xs-1, xs+127): the
+// first tile computes all 18 score rows, later tiles the 16 new ones and carry
+// the two above (and the corners of the last one, an output row of the next
+// tile, in a small list).  Per tile, phases separated by workgroup barriers;
+// the candidate lists are per-wave LDS segments that the next phase reads as
+// one concatenated list in full 64-lane rounds:
 //   compass  every pixel: a run of 9 on the 16-circle contains two adjacent
 //            compass pixels (0,4 / 4,8 / 8,12 / 12,0) that are both brighter
 //            or both darker: min(max(c0,c8), max(c4,c12)) > v+t, or the dual;
@@ -451,8 +457,15 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //   output   keeps per tile row in column order, (offset << 16 | count) per
 //            row; select_fast_kernel restores raster order across tiles.
 constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
-constexpr int kFtRows = 28;                     // staged rows: kBandRows + 8, padded to 4 passes of 7
+constexpr int kFtRows = kBandRows + 8;          // staged image rows per tile: [r0-4, r0+20)
 constexpr int kFtSeg = ((kBandRows + 2 + 3) / 4) * 128;  // per-wave list capacity (score rows sr == wid mod 4)
+constexpr int kFtWords = kFtLW / 4;             // words per staged row
+constexpr int kFtNewW = kBandRows * kFtWords;   // words loaded per tile (rows r0+4 .. r0+20)
+constexpr int kFtPf = (kFtNewW + kFastNT - 1) / kFastNT;
+constexpr int kFtCarryW = 8 * kFtWords;         // image words carried (rows r0+12 .. r0+20 -> top)
+constexpr int kFtCarryR = (kFtCarryW + kFastNT - 1) / kFastNT;
+constexpr int kFtCarryList = 128;               // corners of one score row
+static_assert(kFtRows * kFtWords == kFtNewW + kFtCarryW, "staging covers the window");
 __device__ __forceinline__ uint32_t lane_prefix(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
@@ -469,171 +482,235 @@ __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int 
     return list[s * kFtSeg + e];
 }
 
-__global__ __launch_bounds__(kFastNT) void fast_band_kernel(StreamParams P) {
+__global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     const int f = blockIdx.y;
-    const int item = blockIdx.x;
+    const int strip = blockIdx.x;
     int l = 0;
-    while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].band_base) ++l;
+    while (l + 1 < P.plan.nlevels && strip >= P.plan.L[l + 1].strip_base) ++l;
     const LevelGeom& G = P.plan.L[l];
-    const int t = item - G.band_base;
-    const int b = t / G.ntx, c = t - b * G.ntx;
+    const int c = strip - G.strip_base;
     const int w = G.w, h = G.h;
-    const int r0 = kBorder + b * kBandRows;
-    const int r1 = min(r0 + kBandRows, h - kBorder);
     const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
     const int bx = (xs - 4) & ~3;  // image column of LDS column 0; xs - bx in [4, 7]
     const int thr = P.plan.fast_threshold;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
-    __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];  // rows [r0-4, r1+4) + padding
-    __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];   // rows [r0-1, r1+1)
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
+    __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+20)
+    __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+17)
     __shared__ uint16_t cand[4 * kFtSeg], corner[4 * kFtSeg];
-    __shared__ int ncand[4], ncorner[4];
+    __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
+    __shared__ int ncand[4], ncorner[4], ncarry[2];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
-    __shared__ int row_off[kBandRows];
+    __shared__ int row_off[4][kBandRows];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ylo = r0 - 4, yhi = min(r1 + 4, h);
-    if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
-    {  // stage the window: 7 rows x 36 words per pass, 4 passes, all loads in flight together.
-        // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
-        // load returns whatever lies there (or 0 past the level); rows past yhi go to padding.
-        constexpr int kWords = kFtLW / 4, kPass = kFastNT / kWords, kIters = kFtRows / kPass;
-        const int rr = threadIdx.x / kWords, wd = threadIdx.x - rr * kWords;
-        if (rr < kPass) {
-            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
-            uint32_t v[kIters];
+    const int x_lo = xs - 1 + lane;
+    const int xlast = min(xe, w - 4);  // last score column (xs - 1 >= 30 >= 3 on the left)
+    const bool ok0 = x_lo <= xlast, ok1 = x_lo + 64 <= xlast;
+    // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
+    // load returns whatever lies there (or 0 past the level).
+    uint32_t creg[kFtCarryR], pf[kFtPf], screg = 0;
+    {  // prologue: rows [r0-4, r0+4) into the carry registers, [r0+4, r0+20) into the prefetch registers
+        const int ylo = kBorder - 4;
 #pragma unroll
-            for (int it = 0; it < kIters; ++it) {
-                const int r = min(rr + kPass * it, yhi - ylo - 1);
-                v[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + r) * sp, 0);
-            }
+        for (int k = 0; k < kFtCarryR; ++k) {
+            const int q = threadIdx.x + k * kFastNT;
+            const int rr = q / kFtWords, wd = q - rr * kFtWords;
+            creg[k] = q < kFtCarryW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + rr) * sp, 0) : 0u;
+        }
 #pragma unroll
-            for (int it = 0; it < kIters; ++it) reinterpret_cast<uint32_t*>(img)[(rr + kPass * it) * kWords + wd] = v[it];
+        for (int k = 0; k < kFtPf; ++k) {
+            const int q = threadIdx.x + k * kFastNT;
+            const int rr = q / kFtWords, wd = q - rr * kFtWords;
+            pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + 8 + rr) * sp, 0) : 0u;
         }
     }
-    for (int i = threadIdx.x; i < (kBandRows + 2) * kFtLW / 16; i += kFastNT)
-        reinterpret_cast<uint4*>(sc)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    // ---- compass: score rows sr == wid (mod 4) into this wave's candidate segment
-    const int nsr = r1 - r0 + 2;
-    const int xlast = min(xe, w - 4);  // last score column (xs - 1 >= 30 >= 3 on the left)
-    const int x_lo = xs - 1 + lane;
-    const bool ok0 = x_lo <= xlast, ok1 = x_lo + 64 <= xlast;
-    {
-        uint16_t* seg = cand + wid * kFtSeg;
-        int n = 0;  // wave-uniform
-        for (int sr = wid; sr < nsr; sr += kFastNT / 64) {
-            const int a = (sr + 3) * kFtLW + (x_lo - bx);
+    if (threadIdx.x == 0) ncarry[0] = 0;
+    for (int b = 0; b < G.nbands; ++b) {
+        const int par = b & 1;
+        const int r0 = kBorder + b * kBandRows;
+        const int r1 = min(r0 + kBandRows, h - kBorder);
+        const int nrows = r1 - r0;
+        const int item = G.band_base + b * G.ntx + c;
+        // ---- window: carried rows 0..7, new rows 8..23; score rows 0, 1 carried (tile 0: zero)
 #pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int ah = a + 64 * hh;
-                const int v = img[ah];
-                const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
-                const bool pass = (hh ? ok1 : ok0) &
-                                  ((min(max(c0, c8), max(c4, c12)) > v + thr) | (max(min(c0, c8), min(c4, c12)) < v - thr));
-                const unsigned long long bal = __ballot(pass);
-                if (pass) seg[n + lane_prefix(bal)] = (uint16_t)ah;
+        for (int k = 0; k < kFtCarryR; ++k) {
+            const int q = threadIdx.x + k * kFastNT;
+            if (q < kFtCarryW) reinterpret_cast<uint32_t*>(img)[q] = creg[k];
+        }
+#pragma unroll
+        for (int k = 0; k < kFtPf; ++k) {
+            const int q = threadIdx.x + k * kFastNT;
+            if (q < kFtNewW) reinterpret_cast<uint32_t*>(img)[kFtCarryW + q] = pf[k];
+        }
+        if (threadIdx.x < 2 * kFtWords) reinterpret_cast<uint32_t*>(sc)[threadIdx.x] = b == 0 ? 0u : screg;
+        if (threadIdx.x < kBandRows * kFtLW / 16)
+            reinterpret_cast<uint4*>(sc + 2 * kFtLW)[threadIdx.x] = make_uint4(0, 0, 0, 0);
+        if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+        if (threadIdx.x == 0) ncarry[par ^ 1] = 0;
+        __syncthreads();
+        // ---- next tile: carried rows from LDS, new rows from HBM (in flight during this tile)
+        if (b + 1 < G.nbands) {
+#pragma unroll
+            for (int k = 0; k < kFtCarryR; ++k) {
+                const int q = threadIdx.x + k * kFastNT;
+                creg[k] = q < kFtCarryW ? reinterpret_cast<const uint32_t*>(img)[kFtNewW + q] : 0u;
+            }
+            const int ynew = r0 + kBandRows + 4;
+#pragma unroll
+            for (int k = 0; k < kFtPf; ++k) {
+                const int q = threadIdx.x + k * kFastNT;
+                const int rr = q / kFtWords, wd = q - rr * kFtWords;
+                pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ynew + rr) * sp, 0)
+                                    : 0u;
+            }
+        }
+        // ---- compass: score rows sr == wid (mod 4) into this wave's candidate segment
+        const int nsr = nrows + 2;
+        const int sr_lo = b == 0 ? 0 : 2;
+        {
+            uint16_t* seg = cand + wid * kFtSeg;
+            int n = 0;  // wave-uniform
+            for (int sr = sr_lo + ((wid - sr_lo) & 3); sr < nsr; sr += kFastNT / 64) {
+                const int a = (sr + 3) * kFtLW + (x_lo - bx);
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int ah = a + 64 * hh;
+                    const int v = img[ah];
+                    const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
+#if defined(FAST_EXP) && FAST_EXP == 2
+                    const bool pass = (hh ? ok1 : ok0) & (v > 1000);
+#else
+                    const bool pass = (hh ? ok1 : ok0) &
+                                      ((min(max(c0, c8), max(c4, c12)) > v + thr) | (max(min(c0, c8), min(c4, c12)) < v - thr));
+#endif
+                    const unsigned long long bal = __ballot(pass);
+                    if (pass) seg[n + lane_prefix(bal)] = (uint16_t)ah;
+                    n += __popcll(bal);
+                }
+            }
+            if (lane == 0) ncand[wid] = n;
+        }
+        __syncthreads();
+#if defined(FAST_EXP) && FAST_EXP == 1
+        if (wid == 0 && lane < kBandRows) P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = 0;
+        __syncthreads();
+        continue;
+#endif
+        // ---- segment test over the concatenated candidates, corners into this wave's corner segment
+        {
+            int cnt[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
+            const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+            uint16_t* seg = corner + wid * kFtSeg;
+            int n = 0;
+            for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
+                const int e = e0 + lane;
+                bool is_corner = false;
+                int a = 0;
+                if (e < total) {
+                    a = seg_at(cand, cnt, e);
+                    const uint8_t* p = img + a;
+                    const int v = p[0];
+                    const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
+                    uint32_t br = 0, dk = 0;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
+                        br = __builtin_amdgcn_alignbit(br, hi - cv, 31);  // bit <- (cv > v + thr)
+                        dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);  // bit <- (cv < v - thr)
+                    }
+                    is_corner = has_run9(br) || has_run9(dk);
+                }
+                const unsigned long long bal = __ballot(is_corner);
+                if (is_corner) seg[n + lane_prefix(bal)] = (uint16_t)a;
                 n += __popcll(bal);
             }
+            if (lane == 0) ncorner[wid] = n;
         }
-        if (lane == 0) ncand[wid] = n;
-    }
-    __syncthreads();
-    // ---- segment test over the concatenated candidates, corners into this wave's corner segment
-    {
-        int cnt[4];
+        __syncthreads();
+#if defined(FAST_EXP) && FAST_EXP == 3
+        if (wid == 0 && lane < kBandRows) P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = 0;
+        __syncthreads();
+        continue;
+#endif
+        int cnt2[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
-        const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-        uint16_t* seg = corner + wid * kFtSeg;
-        int n = 0;
-        for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
-            const int e = e0 + lane;
-            bool is_corner = false;
-            int a = 0;
-            if (e < total) {
-                a = seg_at(cand, cnt, e);
-                const uint8_t* p = img + a;
-                const int v = p[0];
-                const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
-                uint32_t br = 0, dk = 0;
+        for (int k = 0; k < 4; ++k) cnt2[k] = ncorner[k];
+        const int ncorners = cnt2[0] + cnt2[1] + cnt2[2] + cnt2[3];
+        const int nc = ncarry[par];
+        // ---- scores of the new corners into the score plane
+        for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
+            const int a = seg_at(corner, cnt2, e);
+            const uint8_t* p = img + a;
+            int cc[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
-                    br = __builtin_amdgcn_alignbit(br, hi - cv, 31);  // bit <- (cv > v + thr)
-                    dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);  // bit <- (cv < v - thr)
-                }
-                is_corner = has_run9(br) || has_run9(dk);
+            for (int k = 0; k < 16; ++k) cc[k] = p[kCdy[k] * kFtLW + kCdx[k]];
+            sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
+        }
+        __syncthreads();
+        // score rows 16, 17 for the next tile (final now)
+        if (threadIdx.x < 2 * kFtWords) screg = reinterpret_cast<const uint32_t*>(sc)[kBandRows * kFtWords + threadIdx.x];
+        // ---- strict 3x3 NMS of the carried and new corners; keeps lie in rows [r0, r1), columns [xs, xe).
+        // New corners of score row 17 (row r0 + 16) are the next tile's row-1 corners.
+        for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
+            const int a = (e < nc ? (int)carry[par][e] : seg_at(corner, cnt2, e - nc)) - 3 * kFtLW;  // score-plane address
+            const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
+            if (sr == kBandRows + 1) {
+                const int slot = atomicAdd(&ncarry[par ^ 1], 1);
+                carry[par ^ 1][slot] = (uint16_t)(a + 3 * kFtLW - kBandRows * kFtLW);
+                continue;
             }
-            const unsigned long long bal = __ballot(is_corner);
-            if (is_corner) seg[n + lane_prefix(bal)] = (uint16_t)a;
-            n += __popcll(bal);
+            if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
+            const uint8_t* s = sc + a;
+            const uint32_t v = s[0];
+            const uint32_t nmax = max(max(max((uint32_t)s[-kFtLW - 1], (uint32_t)s[-kFtLW]),
+                                          max((uint32_t)s[-kFtLW + 1], (uint32_t)s[-1])),
+                                      max(max((uint32_t)s[1], (uint32_t)s[kFtLW - 1]),
+                                          max((uint32_t)s[kFtLW], (uint32_t)s[kFtLW + 1])));
+            if (v > nmax) {
+                const int i_col = x - (xs - 1);
+                atomicOr(&keep[sr - 1][i_col >> 5], 1u << (i_col & 31));
+            }
         }
-        if (lane == 0) ncorner[wid] = n;
-    }
-    __syncthreads();
-    int cnt2[4];
+        __syncthreads();
+        // ---- output: row counts and offsets (a 16-lane scan in every wave), then every kept corner
+        // writes its key at row offset + kept columns before it: keys of a row land in column order
+        uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off +
+                         (int64_t)(b * G.ntx + c) * G.band_cap;
+        {
+            int rc = 0;
+            if (lane < kBandRows && lane < nrows)
+                rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
+            int incl = rc;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) cnt2[k] = ncorner[k];
-    const int ncorners = cnt2[0] + cnt2[1] + cnt2[2] + cnt2[3];
-    // ---- scores of the corners into the score plane
-    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
-        const int a = seg_at(corner, cnt2, e);
-        const uint8_t* p = img + a;
-        int cc[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) cc[k] = p[kCdy[k] * kFtLW + kCdx[k]];
-        sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
-    }
-    __syncthreads();
-    // ---- strict 3x3 NMS of the corners; keeps lie in rows [r0, r1), columns [xs, xe)
-    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
-        const int a = seg_at(corner, cnt2, e) - 3 * kFtLW;  // score-plane address
-        const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
-        if (sr < 1 || sr > r1 - r0 || x < xs || x >= xe) continue;
-        const uint8_t* s = sc + a;
-        const uint32_t v = s[0];
-        const uint32_t nmax = max(max(max((uint32_t)s[-kFtLW - 1], (uint32_t)s[-kFtLW]),
-                                      max((uint32_t)s[-kFtLW + 1], (uint32_t)s[-1])),
-                                  max(max((uint32_t)s[1], (uint32_t)s[kFtLW - 1]),
-                                      max((uint32_t)s[kFtLW], (uint32_t)s[kFtLW + 1])));
-        if (v > nmax) {
-            const int i_col = x - (xs - 1);
-            atomicOr(&keep[sr - 1][i_col >> 5], 1u << (i_col & 31));
+            for (int o = 1; o < kBandRows; o <<= 1) {
+                const int y2 = __shfl_up(incl, o);
+                if (lane >= o) incl += y2;
+            }
+            if (lane < kBandRows) {
+                row_off[wid][lane] = incl - rc;
+                if (wid == 0)
+                    P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = ((incl - rc) << 16) | rc;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-    }
-    __syncthreads();
-    // ---- output: row counts and offsets (one 16-lane scan), then every kept corner writes its key
-    // at row offset + kept columns before it: keys of a row land in column order
-    uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off + (int64_t)t * G.band_cap;
-    const int nrows = r1 - r0;
-    if (wid == 0) {
-        int rc = 0;
-        if (lane < kBandRows && lane < nrows)
-            rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
-        int incl = rc;
-#pragma unroll
-        for (int o = 1; o < kBandRows; o <<= 1) {
-            const int y2 = __shfl_up(incl, o);
-            if (lane >= o) incl += y2;
+        for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
+            const int a = (e < nc ? (int)carry[par][e] : seg_at(corner, cnt2, e - nc)) - 3 * kFtLW;
+            const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
+            if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
+            const int i_col = x - (xs - 1), wq = i_col >> 5;
+            const uint32_t* kr = keep[sr - 1];
+            if (!((kr[wq] >> (i_col & 31)) & 1)) continue;
+            int before = __popc(kr[wq] & ((1u << (i_col & 31)) - 1));
+            for (int q = 0; q < wq; ++q) before += __popc(kr[q]);
+            outp[row_off[wid][sr - 1] + before] = ((uint32_t)sc[a] << 24) | ((uint32_t)(r0 + sr - 1) << 12) | (uint32_t)x;
         }
-        if (lane < kBandRows) {
-            row_off[lane] = incl - rc;
-            P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = ((incl - rc) << 16) | rc;
-        }
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
-        const int a = seg_at(corner, cnt2, e) - 3 * kFtLW;
-        const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
-        if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
-        const int i_col = x - (xs - 1), w = i_col >> 5;
-        const uint32_t* kr = keep[sr - 1];
-        if (!((kr[w] >> (i_col & 31)) & 1)) continue;
-        int before = __popc(kr[w] & ((1u << (i_col & 31)) - 1));
-        for (int q = 0; q < w; ++q) before += __popc(kr[q]);
-        outp[row_off[sr - 1] + before] = ((uint32_t)sc[a] << 24) | ((uint32_t)(r0 + sr - 1) << 12) | (uint32_t)x;
+        __syncthreads();
     }
 }
 
@@ -1238,8 +1315,8 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
-    if (pl.total_bands > 0)
-        hipLaunchKernelGGL(fast_band_kernel, dim3(pl.total_bands, F), dim3(kFastNT), 0, s, P);
+    if (pl.total_strips > 0)
+        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips, F), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
