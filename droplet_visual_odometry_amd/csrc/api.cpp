@@ -246,10 +246,14 @@ GeomArgs stream_geom(dvo_stream* s) {
     g.dk_off = s->buf.dk_off;
     g.dk_ctl = s->buf.dk_ctl;
     g.hyp_cap = c.max_iters > 1 ? c.max_iters : 1;
+    g.dk_list = s->buf.dk_list;
+    g.dk_list_cap = (int64_t)s->cfg.max_frames * g.hyp_cap;
     g.E = s->buf.E;
     g.info = s->buf.info;
     g.Rt = s->buf.Rt;
     g.good = s->buf.good;
+    g.pose_P = s->buf.pose_P;
+    g.pose_cnt = s->buf.pose_cnt;
     return g;
 }
 
@@ -295,12 +299,15 @@ int stream_alloc(dvo_stream* s) {
     A(b.gscr, (size_t)F * ((hc + 63) / 64) * 200 * 64);
     A(b.fprec, (size_t)F * ((hc + 63) / 64) * 128 * 64);
     A(b.dk_off, (size_t)F + 1);
-    A(b.dk_ctl, (size_t)2);
+    A(b.dk_ctl, (size_t)4);
+    A(b.dk_list, (size_t)2 * F * hc);
     A(b.status, (size_t)F);
     A(b.E, (size_t)F * 90);
     A(b.info, (size_t)F * 4);
     A(b.Rt, (size_t)F * 12);
     A(b.good, (size_t)F);
+    A(b.pose_P, (size_t)F * 72);
+    A(b.pose_cnt, (size_t)F * 5);
     A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
     A(s->d_carry, (size_t)28);
 #undef A
@@ -702,7 +709,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     if (!(prob > 0 && prob < 1)) return fail(ctx, DVO_EINVAL, "prob must be in (0, 1)");
     if (m < 5) return fail(ctx, DVO_EFEWPTS, "fewer than 5 correspondences");
     HIP_TRY(hipSetDevice(ctx->device));
-    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *dgs, *drec, *doff, *dctl;
+    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *dgs, *drec, *doff, *dctl, *dlist;
     int rc;
     const size_t hc = (size_t)(max_iters > 1 ? max_iters : 1);
     if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)m * 32, &dn)) ||
@@ -712,7 +719,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 20, ((hc + 63) / 64) * 200 * 64 * 8, &dgs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
-        (rc = scratch(ctx, 23, 8, &dctl)))
+        (rc = scratch(ctx, 23, 16, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)))
         return rc;
     GeomArgs g{};
     g.pts_d = (const double*)dpts;
@@ -735,6 +742,8 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.fprec = (double*)drec;
     g.dk_off = (int32_t*)doff;
     g.dk_ctl = (int32_t*)dctl;
+    g.dk_list = (int32_t*)dlist;
+    g.dk_list_cap = (int64_t)hc;
     g.hyp_cap = (int)hc;
     g.E = (double*)dE;
     g.info = (int32_t*)dinfo;
@@ -789,6 +798,10 @@ int dvo_recover_pose(dvo_ctx* ctx, const double* E, int e_rows, const double* p1
     g.good = (int32_t*)dgood;
     g.pick = (int32_t*)dpick;
     g.pose_mask = (uint8_t*)dpm;
+    void *dpP, *dpc;
+    if ((rc = scratch(ctx, 25, 72 * sizeof(double), &dpP)) || (rc = scratch(ctx, 26, 5 * sizeof(int32_t), &dpc))) return rc;
+    g.pose_P = (double*)dpP;
+    g.pose_cnt = (int32_t*)dpc;
     HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStagePose, ctx->stream));
     double Rt[12];
     int gd = 0, pick = 0;

@@ -108,12 +108,15 @@ struct Buffers {
     double* gscr;         // [F][ceil(hyp_cap / 64)][200][64]
     double* fprec;        // [F][ceil(hyp_cap / 64)][128][64]
     int32_t* dk_off;      // [F + 1]
-    int32_t* dk_ctl;      // [2]
+    int32_t* dk_ctl;      // [4]
+    int32_t* dk_list;     // [2][F * hyp_cap] parked Durand-Kerner polynomials
     int32_t* status;      // [F] per-frame error flags
     double* E;            // [F][90]
     int32_t* info;        // [F][4] rows, inliers, iters, status
     double* Rt;           // [F][12]
     int32_t* good;        // [F]
+    double* pose_P;       // [F][72] recoverPose decompositions (4 P, R1, R2, t)
+    int32_t* pose_cnt;    // [F][5] decomposition valid flag, cheirality counts
 };
 
 
@@ -163,7 +166,9 @@ struct GeomArgs {
     double* gscr;           // [pairs][ceil(hyp_cap / 64)][200][64] five-point scratch
     double* fprec;          // [pairs][ceil(hyp_cap / 64)][128][64] five-point records
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
-    int32_t* dk_ctl;        // [2] queue head, total
+    int32_t* dk_ctl;        // [4] -, pass-0 items, parked after pass 0, parked after pass 1
+    int32_t* dk_list;       // [2][dk_list_cap] parked polynomials (work-list items)
+    int64_t dk_list_cap;    // >= pairs * hyp_cap
     int hyp_cap;            // max(max_iters, 1)
     double* E;              // [pairs][90]
     int32_t* info;          // [pairs][4] rows, inliers, iters, status
@@ -173,6 +178,8 @@ struct GeomArgs {
     int32_t* good;          // [pairs]
     int32_t* pick;          // [pairs] chosen decomposition 0..3, or null
     uint8_t* pose_mask;     // [pairs][pts_stride][4] per-decomposition masks, or null
+    double* pose_P;         // [pairs][72] decompositions [R1|t], [R2|t], [R1|-t], [R2|-t]; R1, R2, t
+    int32_t* pose_cnt;      // [pairs][5] valid flag, cheirality counts of the 4 decompositions
 };
 
 constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;

@@ -14,7 +14,8 @@
 // the round in iteration order, stopping where OpenCV would.  The result is
 // identical to the sequential loop; only iterations past OpenCV's stop are
 // wasted.
-// recover_pose_kernel: one workgroup per pair; thread 0 decomposes E, all
+// pose_decompose/count/pick kernels (recoverPose): per pair decomposition, then one thread per
+// (point, decomposition); formerly: one workgroup per pair; thread 0 decomposes E, all
 // threads triangulate (4 poses x M points, one 4x4 Jacobi SVD per item).
 //
 // Every double expression mirrors oracle/geometry.cpp operation for operation
@@ -1090,7 +1091,9 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
     if (threadIdx.x == 0) {
         g.dk_off[pairs] = s_carry;
         g.dk_ctl[0] = 0;
-        g.dk_ctl[1] = s_carry;
+        g.dk_ctl[1] = s_carry;  // pass 0 items
+        g.dk_ctl[2] = 0;        // parked after pass 0
+        g.dk_ctl[3] = 0;        // parked after pass 1
     }
 }
 
@@ -1116,53 +1119,80 @@ __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
     fp_stage_a(q, lds_g + threadIdx.x, gg, hyp_record(g, p, h));
 }
 
-// Durand-Kerner for every polynomial of the round: persistent lanes pull
-// polynomials from a queue, so a lane whose roots settle early (Brent) takes
-// the next one instead of idling until the slowest lane of its wave is done.
-constexpr int kDkNT = 256, kDkBlocks = 1024;
-__global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8))) void ransac_dk_kernel(GeomArgs g, int pairs) {
-    const int total = g.dk_ctl[1];
+// Durand-Kerner for every polynomial of the round, in passes that shrink the
+// set of waves holding the long tail.  A pass gives every listed polynomial
+// one lane and at most `budget` sweeps; polynomials still running then (a long
+// pre-period or period before Brent's exit, or no cycle within 300 sweeps:
+// ~40% after 48 sweeps, ~20% after 128) park their state in their record -
+// roots, Brent snapshot and counters - and join the next pass's list.  The
+// sweeps are the same deterministic map whichever pass runs them, so the
+// roots are bit-identical to one uninterrupted run; the tail just no longer
+// keeps every wave of the round resident (it needed all of them for ~300
+// sweeps before).
+constexpr int kDkNT = 256;
+constexpr int kDkBudget0 = 48, kDkBudget1 = 80;  // sweeps of passes 0 and 1; pass 2 runs to the end
+constexpr int kRecSnap = 108;                     // parked: Brent snapshot (20 doubles)
+__global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
+void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
+    // pass 0: items [0, dk_ctl[1]) of the round's work list; pass k > 0: dk_list[k - 1][0, dk_ctl[1 + k])
+    const int total = g.dk_ctl[1 + pass];
     if ((int)blockIdx.x * kDkNT >= total) return;
     __shared__ double s_saved[20 * kDkNT];
-    int item = -1;
+    const int e = blockIdx.x * kDkNT + threadIdx.x;
+    if (e >= total) return;
+    const int item = pass == 0 ? e : g.dk_list[(int64_t)(pass - 1) * g.dk_list_cap + e];
+    int lo = 0, hi = pairs - 1;  // pair p with off[p] <= item < off[p + 1]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (g.dk_off[mid] <= item) lo = mid;
+        else hi = mid - 1;
+    }
+    double* R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
+    if (pass == 0 && R[kRecGeneric * 64] != 0.0) return;  // stage C runs the generic solver
     double c[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
     Cx roots[10];
     DkBrent br;
     br.saved = s_saved + threadIdx.x;
     br.stride = kDkNT;
-    double* R = nullptr;
-    for (;;) {
-        while (item < 0) {
-            item = atomicAdd(&g.dk_ctl[0], 1);
-            if (item >= total) break;
-            int lo = 0, hi = pairs - 1;  // pair p with off[p] <= item < off[p + 1]
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (g.dk_off[mid] <= item) lo = mid;
-                else hi = mid - 1;
-            }
-            R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
-            if (R[kRecGeneric * 64] != 0.0) {  // stage C runs the generic solver
-                item = -1;
-                continue;
+    if (pass == 0) {
+        dk_init(roots);
+        br.start(roots);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 10; i++) roots[i] = Cx{R[(kRecRoots + 2 * i) * 64], R[(kRecRoots + 2 * i + 1) * 64]};
+#pragma unroll
+        for (int k = 0; k < 20; ++k) br.saved[k * br.stride] = R[(kRecSnap + k) * 64];
+        const int pk = (int)R[kRecNr * 64];
+        br.it = pk & 511;
+        br.saved_it = (pk >> 9) & 511;
+        br.power = 1 << ((pk >> 18) & 15);
+        br.target = (pk >> 22) & 511;
+    }
+    for (int sweep = 0;; ++sweep) {
+        if (sweep == budget) {  // park for the next pass
+#pragma unroll
+            for (int i = 0; i < 10; i++) {
+                R[(kRecRoots + 2 * i) * 64] = roots[i].re;
+                R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
             }
 #pragma unroll
-            for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
-            dk_init(roots);
-            br.start(roots);
+            for (int k = 0; k < 20; ++k) R[(kRecSnap + k) * 64] = br.saved[k * br.stride];
+            R[kRecNr * 64] = (double)(br.it | br.saved_it << 9 | (31 - __clz(br.power)) << 18 | br.target << 22);
+            const int slot = atomicAdd(&g.dk_ctl[2 + pass], 1);
+            g.dk_list[(int64_t)pass * g.dk_list_cap + slot] = item;
+            return;
         }
-        const bool active = item >= 0 && item < total;
-        if (__ballot(active) == 0) break;
-        if (active) {
-            bool moved, same = false;
-            dk_sweep<false>(c, roots, moved, same);
-            if (same) {  // coincident roots: stage C redoes this polynomial exactly
-                R[kRecGeneric * 64] = 2.0;
-                item = -1;
-            } else if (br.step(roots, moved)) {
-                dk_store(R, roots);
-                item = -1;
-            }
+        bool moved, same = false;
+        dk_sweep<false>(c, roots, moved, same);
+        if (same) {  // coincident roots: stage C redoes this polynomial exactly
+            R[kRecGeneric * 64] = 2.0;
+            return;
+        }
+        if (br.step(roots, moved)) {
+            dk_store(R, roots);
+            return;
         }
     }
 }
@@ -1339,7 +1369,10 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
         const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
         hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
         hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        hipLaunchKernelGGL(ransac_dk_kernel, dim3(kDkBlocks), dim3(kDkNT), 0, s, g, pairs);
+        const dim3 dgrid((unsigned)(((int64_t)pairs * span + kDkNT - 1) / kDkNT));
+        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 0, kDkBudget0);
+        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
+        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
         hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
         hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
                            s, g);
@@ -1383,108 +1416,117 @@ __device__ __forceinline__ void triangulate_one(const double* P1, const double* 
     for (int k = 0; k < 4; ++k) X[k] = Vt[3][k];
 }
 
+// recoverPose in three launches: decomposeEssentialMat per pair (one thread
+// each), then one thread per (point, decomposition) - 4M DLT triangulations
+// per pair, a 4x4 Jacobi SVD each, spread over the whole GPU instead of one
+// workgroup per pair - with per-wave ballot counts added into the pair's four
+// totals (integers: order-free), then the tie-ordered pick.
 constexpr int kPNT = 256;
+constexpr int kPoseRec = 72;  // per pair: 4 P (3x4), R1, R2, t
 
-__global__ __launch_bounds__(kPNT) void recover_pose_kernel(GeomArgs g) {
-    const int p = blockIdx.x;
-    const int m = pair_m(g, p);
-    const int tid = threadIdx.x;
-    __shared__ double sP[4][12];
-    __shared__ double sR[2][9];
-    __shared__ double st[3];
-    __shared__ int s_good[4];
-    __shared__ int s_ok;
+// P of decomposition c (row-major 3x4) from the pair's record: [R1|t], [R2|t], [R1|-t], [R2|-t]
+__global__ __launch_bounds__(64) void pose_decompose_kernel(GeomArgs g, int pairs) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= pairs) return;
     const int32_t* info = g.info + (int64_t)p * 4;
-    if (tid == 0) {
-        s_ok = info[3] == DVO_OK && info[0] == 3;
-        for (int c = 0; c < 4; ++c) s_good[c] = 0;
-        if (s_ok) {
-            const double* E = g.E + (int64_t)p * 90;
-            double At[3][3], W[3], Vt[3][3], U[3][3];
-            for (int r = 0; r < 3; ++r)
-                for (int k = 0; k < 3; ++k) At[r][k] = E[k * 3 + r];
-            jacobi_svd<3, 3, 3, 3>(At, W, Vt);
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 3; ++c) U[r][c] = At[c][r];
-            if (det3(U) < 0)
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) U[r][c] *= -1.;
-            if (det3(Vt) < 0)
-                for (int r = 0; r < 3; ++r)
-                    for (int c = 0; c < 3; ++c) Vt[r][c] *= -1.;
-            const double Wm[3][3] = {{0, 1, 0}, {-1, 0, 0}, {0, 0, 1}};
-            const double Wt[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
-            double UW[3][3], R1[3][3], R2[3][3];
-            matmul3(U, Wm, UW);
-            matmul3(UW, Vt, R1);
-            matmul3(U, Wt, UW);
-            matmul3(UW, Vt, R2);
-            double tv[3];
-            for (int k = 0; k < 3; ++k) tv[k] = U[k][2] + 0.0;
-            for (int r = 0; r < 3; ++r)
-                for (int k = 0; k < 3; ++k) {
-                    sR[0][r * 3 + k] = R1[r][k];
-                    sR[1][r * 3 + k] = R2[r][k];
-                }
-            for (int k = 0; k < 3; ++k) st[k] = tv[k];
-            for (int c = 0; c < 4; ++c) {
-                const double* Rs = sR[c & 1];
-                for (int r = 0; r < 3; ++r) {
-                    for (int k = 0; k < 3; ++k) sP[c][r * 4 + k] = Rs[r * 3 + k] + 0.0;
-                    sP[c][r * 4 + 3] = c < 2 ? tv[r] + 0.0 : 0.0 - tv[r];
-                }
-            }
+    int32_t* cnt = g.pose_cnt + (int64_t)p * 5;
+    const bool ok = info[3] == DVO_OK && info[0] == 3;
+    cnt[0] = ok;
+    for (int c = 0; c < 4; ++c) cnt[1 + c] = 0;
+    if (!ok) return;
+    const double* E = g.E + (int64_t)p * 90;
+    double At[3][3], W[3], Vt[3][3], U[3][3];
+    for (int r = 0; r < 3; ++r)
+        for (int k = 0; k < 3; ++k) At[r][k] = E[k * 3 + r];
+    jacobi_svd<3, 3, 3, 3>(At, W, Vt);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) U[r][c] = At[c][r];
+    if (det3(U) < 0)
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) U[r][c] *= -1.;
+    if (det3(Vt) < 0)
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) Vt[r][c] *= -1.;
+    const double Wm[3][3] = {{0, 1, 0}, {-1, 0, 0}, {0, 0, 1}};
+    const double Wt[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+    double UW[3][3], R1[3][3], R2[3][3];
+    matmul3(U, Wm, UW);
+    matmul3(UW, Vt, R1);
+    matmul3(U, Wt, UW);
+    matmul3(UW, Vt, R2);
+    double* P = g.pose_P + (int64_t)p * kPoseRec;
+    for (int k = 0; k < 9; ++k) {  // the unnormalised R1, R2, t recoverPose returns
+        P[48 + k] = R1[k / 3][k % 3];
+        P[57 + k] = R2[k / 3][k % 3];
+    }
+    for (int k = 0; k < 3; ++k) P[66 + k] = U[k][2] + 0.0;
+    for (int c = 0; c < 4; ++c) {
+        const double(&Rs)[3][3] = (c & 1) ? R2 : R1;
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k) P[c * 12 + r * 4 + k] = Rs[r][k] + 0.0;
+            const double tv = U[r][2] + 0.0;
+            P[c * 12 + r * 4 + 3] = c < 2 ? tv + 0.0 : 0.0 - tv;
         }
     }
-    __syncthreads();
-    if (!s_ok) {
-        if (tid == 0) {
-            g.good[p] = 0;
-            if (g.pick) g.pick[p] = -1;
-        }
-        return;
-    }
-    const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
-    const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
-    int cnt[4] = {0, 0, 0, 0};
-    for (int w = tid; w < 4 * m; w += kPNT) {
-        const int c = w & 3, i = w >> 2;
-        const double* pt = npts + (int64_t)i * 4;
+}
+
+__global__ __launch_bounds__(kPNT) void pose_count_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    int32_t* cnt = g.pose_cnt + (int64_t)p * 5;
+    if (!cnt[0]) return;
+    const int m = pair_m(g, p);
+    const int w = blockIdx.x * kPNT + threadIdx.x;
+    if ((int)blockIdx.x * kPNT >= 4 * m) return;
+    const int c = w & 3, i = w >> 2;
+    bool ok = false;
+    if (i < m) {
+        const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+        const double* Pc = g.pose_P + (int64_t)p * kPoseRec + c * 12;
+        double Pl[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Pl[k] = Pc[k];
+        const double* pt = g.npts + ((int64_t)p * g.pts_stride + i) * 4;
         double X[4];
-        triangulate_one(P0, sP[c], pt[0], pt[1], pt[2], pt[3], X);
-        bool ok = X[2] * X[3] > 0;
+        triangulate_one(P0, Pl, pt[0], pt[1], pt[2], pt[3], X);
+        ok = X[2] * X[3] > 0;
         double q0 = X[0] / X[3], q1 = X[1] / X[3], q2 = X[2] / X[3], q3 = X[3] / X[3];
         ok = (q2 < g.dist_thresh) && ok;
-        const double* Pr = sP[c] + 8;
-        double z = Pr[0] * q0 + Pr[1] * q1 + Pr[2] * q2 + Pr[3] * q3;
+        double z = Pl[8] * q0 + Pl[9] * q1 + Pl[10] * q2 + Pl[11] * q3;
         ok = (z > 0) && ok;
         ok = (z < g.dist_thresh) && ok;
         uint8_t mv = ok ? 255 : 0;
         if (g.mask_in) mv &= g.mask_in[(int64_t)p * g.pts_stride + i];  // bitwise_and(mask, mask_c)
-        if (mv) cnt[c]++;
+        ok = mv != 0;
         if (g.pose_mask) g.pose_mask[((int64_t)p * g.pts_stride + i) * 4 + c] = mv;
     }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int v = cnt[c];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if ((tid & 63) == 0) atomicAdd(&s_good[c], v);
+    const unsigned long long bal = __ballot(ok);  // lane l holds decomposition l & 3
+    if ((threadIdx.x & 63) < 4) {
+        const int n = __popcll(bal & (0x1111111111111111ull << (threadIdx.x & 3)));
+        if (n) atomicAdd(&cnt[1 + (threadIdx.x & 3)], n);
     }
-    __syncthreads();
-    if (tid == 0) {
-        const int* gd = s_good;
-        int pick;
-        if (gd[0] >= gd[1] && gd[0] >= gd[2] && gd[0] >= gd[3]) pick = 0;
-        else if (gd[1] >= gd[0] && gd[1] >= gd[2] && gd[1] >= gd[3]) pick = 1;
-        else if (gd[2] >= gd[0] && gd[2] >= gd[1] && gd[2] >= gd[3]) pick = 2;
-        else pick = 3;
-        double* Rt = g.Rt + (int64_t)p * 12;
-        for (int k = 0; k < 9; ++k) Rt[k] = sR[pick & 1][k];
-        for (int k = 0; k < 3; ++k) Rt[9 + k] = pick < 2 ? st[k] : 0.0 - st[k];
-        g.good[p] = gd[pick];
-        if (g.pick) g.pick[p] = pick;
+}
+
+__global__ __launch_bounds__(64) void pose_pick_kernel(GeomArgs g, int pairs) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= pairs) return;
+    const int32_t* cnt = g.pose_cnt + (int64_t)p * 5;
+    if (!cnt[0]) {
+        g.good[p] = 0;
+        if (g.pick) g.pick[p] = -1;
+        return;
     }
+    const int* gd = cnt + 1;
+    int pick;
+    if (gd[0] >= gd[1] && gd[0] >= gd[2] && gd[0] >= gd[3]) pick = 0;
+    else if (gd[1] >= gd[0] && gd[1] >= gd[2] && gd[1] >= gd[3]) pick = 1;
+    else if (gd[2] >= gd[0] && gd[2] >= gd[1] && gd[2] >= gd[3]) pick = 2;
+    else pick = 3;
+    const double* P = g.pose_P + (int64_t)p * kPoseRec;
+    double* Rt = g.Rt + (int64_t)p * 12;
+    for (int k = 0; k < 9; ++k) Rt[k] = P[(pick & 1 ? 57 : 48) + k];
+    for (int k = 0; k < 3; ++k) Rt[9 + k] = pick < 2 ? P[66 + k] : 0.0 - P[66 + k];
+    g.good[p] = gd[pick];
+    if (g.pick) g.pick[p] = pick;
 }
 
 __global__ void triangulate_kernel(const double* P, const double* x, int k, double* X) {
@@ -1699,7 +1741,12 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
         hipError_t e = launch_ransac(g, pairs, s);
         if (e != hipSuccess) return e;
     }
-    if (stages & kStagePose) hipLaunchKernelGGL(recover_pose_kernel, dim3(pairs), dim3(kPNT), 0, s, g);
+    if (stages & kStagePose) {
+        hipLaunchKernelGGL(pose_decompose_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs);
+        hipLaunchKernelGGL(pose_count_kernel, dim3((unsigned)((4 * g.pts_stride + kPNT - 1) / kPNT), pairs), dim3(kPNT), 0,
+                           s, g);
+        hipLaunchKernelGGL(pose_pick_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs);
+    }
     return hipGetLastError();
 }
 
