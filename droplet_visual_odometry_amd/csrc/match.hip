@@ -184,31 +184,74 @@ __global__ __launch_bounds__(kFNT) void nn_fused_kernel(StreamParams P) {
 }
 
 // Forward + backward nearest neighbours of one stream pair on the matrix cores.
-// With descriptor bits as +-1 bytes (desc_x, written by describe_kernel), the
-// 256-term dot product s = q.t = 256 - 2 * Hamming(q, t) is an int8 GEMM:
-// v_mfma_i32_32x32x32_i8, 8 k-steps per 32x32 tile, exact in int32.  A wave
-// owns 64 queries (two 32-row strips, A fragments resident in VGPRs); the
-// workgroup streams the trains through LDS 64 at a time (16-byte chunks XOR-
-// swizzled by train so the b128 fragment reads are conflict-free).  From each
-// tile: key = (Hamming << 16) | index = (256 << 15) + index - s * 2^15, one
-// v_mad_i32_i24 per element; forward keys fold into a per-register running
-// minimum (the lane's column changes, its rows do not), backward keys fold
-// over the lane's 16 rows and into LDS / global atomicMin.  Minimum packed keys
-// give OpenCV's first-index tie rule exactly as the VALU kernels do.
+// Descriptor bits are +-1 bytes (desc_x, written by describe_kernel); scaled
+// on the way into registers / LDS to +64 (queries) and -64 (trains), the
+// v_mfma_i32_32x32x32_i8 accumulator is D = -4096 s where s = q.t = 256 -
+// 2 * Hamming(q, t), exact in int32.  Then key = 2^20 + D + index =
+// Hamming * 8192 + index (index < 8192): one add per element and direction,
+// and the minimum key is OpenCV's nearest neighbour with its first-index tie
+// rule.  A wave owns 64 queries (two 32-row strips, A fragments resident in
+// VGPRs); the workgroup streams the trains through LDS 64 at a time, double-
+// buffered (the next stage's global loads are in flight during this stage's
+// MFMAs; one barrier per stage), 16-byte chunks XOR-swizzled by train so the
+// b128 fragment reads are conflict-free.  Forward keys fold into a per-
+// register running minimum (the lane's column changes, its rows do not);
+// backward keys fold over the lane's 32 rows (v_min3), into LDS, then a global
+// atomicMin per train in the (Hamming << 16 | index) form the cross check
+// reads (the re-encoding is monotone, so the minimum is the same).  Workgroups
+// are grouped by XCD (blocks b and b + 8 share one) so the query blocks of a
+// pair stream its trains through one L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kMWaves = 4, kMQB = 64 * kMWaves, kMStage = 64;
-constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^25), < 0x7F7F7F7F
+constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^22), < 0x7F7F7F7F
+constexpr int kKeyBase = 1 << 20;     // 256 * 4096
 
-__device__ __forceinline__ int key_of(int s, int c) { return __mul24(s, -32768) + c; }
+__device__ __forceinline__ v4i scale_q(v4i x) { return (x & 0x03030303) << 6; }                 // +-1 -> +-64
+__device__ __forceinline__ v4i scale_t(v4i x) { return ((x & 0x03030303) << 6) ^ (int)0x80808080; }  // +-1 -> -+64
+__device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 8191); }
 
-__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P) {
-    __shared__ v4i bt[kMStage * 16];
-    __shared__ int colmin[kMStage];
-    const int p = blockIdx.y;
+template <bool kFull>
+__device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][8], int (&best)[2][16], int t0,
+                                         int nt, int r, int h, int rowb, int nq) {
+#pragma unroll 1
+    for (int tt = 0; tt < kMStage / 32; ++tt) {
+        const int j = t0 + 32 * tt + r;
+        const int cf = j < nt ? kKeyBase + j : kKeyNone;
+        v16i acc0 = {}, acc1 = {};
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const v4i B = btc[(32 * tt + r) * 16 + ((2 * ks + h) ^ (r & 15))];
+            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][ks], B, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1][ks], B, acc1, 0, 0, 0);
+        }
+        int cm = 0x7FFFFFFF;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int goff = (g & 3) + 8 * (g >> 2);
+            best[0][g] = min(best[0][g], acc0[g] + cf);
+            best[1][g] = min(best[1][g], acc1[g] + cf);
+            int k0 = acc0[g] + (rowb + goff), k1 = acc1[g] + (rowb + 32 + goff);
+            if (!kFull) {
+                k0 = rowb - kKeyBase + goff < nq ? k0 : kKeyNone;
+                k1 = rowb - kKeyBase + 32 + goff < nq ? k1 : kKeyNone;
+            }
+            cm = min(cm, min(k0, k1));
+        }
+        if (j < nt) atomicMin(&cmin[32 * tt + r], cm);
+    }
+}
+
+__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs, int nqb) {
+    __shared__ v4i bt[2][kMStage * 16];
+    __shared__ int colmin[2][kMStage];
+    const int nwg = gridDim.x;  // a multiple of 8
+    const int L = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+    const int p = L / nqb, qb = L - p * nqb;
+    if (p >= pairs) return;
     const int cap = P.plan.kp_cap;
     const int nq = min(P.buf.nkp[p], cap), nt = min(P.buf.nkp[p + 1], cap);
-    const int qbase = blockIdx.x * kMQB;
+    const int qbase = qb * kMQB;
     if (qbase >= nq) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -223,70 +266,56 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P) {
     for (int s2 = 0; s2 < 2; ++s2) {
         const int q = qs + 32 * s2 + r;
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) A[s2][ks] = q < nq ? XQ[(int64_t)q * 16 + 2 * ks + h] : (v4i){0, 0, 0, 0};
+        for (int ks = 0; ks < 8; ++ks) A[s2][ks] = q < nq ? scale_q(XQ[(int64_t)q * 16 + 2 * ks + h]) : (v4i){0, 0, 0, 0};
 #pragma unroll
         for (int g = 0; g < 16; ++g) best[s2][g] = 0x7FFFFFFF;
     }
-    // backward key base of register g: (256 << 15) + row(g); rows past nq never win (partial waves only)
-    const int cb0 = (256 << 15) + qs + 4 * h;
+    // backward key base of register g: 2^20 + row(g); rows past nq never win (partial waves only)
+    const int rowb = kKeyBase + qs + 4 * h;
     const bool full = qs + 64 <= nq;
-    for (int t0 = 0; t0 < nt; t0 += kMStage) {
-        __syncthreads();
-        {  // 4 chunks per thread, all loads in flight (clamped index, zeroed past nt)
-            v4i v[kMStage * 16 / 256];
+    const int nst = (nt + kMStage - 1) / kMStage;
+    v4i v[kMStage * 16 / 256];
+    auto load_stage = [&](int st) {  // 4 chunks per thread (clamped index; zeroed past nt when stored)
 #pragma unroll
-            for (int it = 0; it < kMStage * 16 / 256; ++it) {
-                const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
-                v[it] = XT[(int64_t)min(t0 + tr, nt - 1) * 16 + c];
-            }
-#pragma unroll
-            for (int it = 0; it < kMStage * 16 / 256; ++it) {
-                const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
-                bt[tr * 16 + (c ^ (tr & 15))] = t0 + tr < nt ? v[it] : (v4i){0, 0, 0, 0};
-            }
+        for (int it = 0; it < kMStage * 16 / 256; ++it) {
+            const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
+            v[it] = XT[(int64_t)min(st * kMStage + tr, nt - 1) * 16 + c];
         }
-        if (threadIdx.x < kMStage) colmin[threadIdx.x] = 0x7FFFFFFF;
-        __syncthreads();
-#pragma unroll 1
-        for (int tt = 0; tt < kMStage / 32; ++tt) {
-            const int j = t0 + 32 * tt + r;
-            const int cf = j < nt ? (256 << 15) + j : kKeyNone;
-            v16i acc0 = {}, acc1 = {};
+    };
+    auto store_stage = [&](int st, int b) {
 #pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {
-                const v4i B = bt[(32 * tt + r) * 16 + ((2 * ks + h) ^ (r & 15))];
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][ks], B, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1][ks], B, acc1, 0, 0, 0);
-            }
-            int cm = 0x7FFFFFFF;
-#pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const int goff = (g & 3) + 8 * (g >> 2);
-                best[0][g] = min(best[0][g], key_of(acc0[g], cf));
-                best[1][g] = min(best[1][g], key_of(acc1[g], cf));
-                int k0 = key_of(acc0[g], cb0 + goff), k1 = key_of(acc1[g], cb0 + 32 + goff);
-                if (!full) {
-                    k0 = qs + 4 * h + goff < nq ? k0 : kKeyNone;
-                    k1 = qs + 32 + 4 * h + goff < nq ? k1 : kKeyNone;
-                }
-                cm = min(cm, min(k0, k1));
-            }
-            if (cm < kKeyNone && j < nt) atomicMin(&colmin[32 * tt + r], cm);
+        for (int it = 0; it < kMStage * 16 / 256; ++it) {
+            const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
+            bt[b][tr * 16 + (c ^ (tr & 15))] = st * kMStage + tr < nt ? scale_t(v[it]) : (v4i){0, 0, 0, 0};
         }
+        if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;
+    };
+    if (nst > 0) {
+        load_stage(0);
+        store_stage(0, 0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < nst) load_stage(st + 1);
+        if (full) nn_stage<true>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
+        else nn_stage<false>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
+        if (st + 1 < nst) store_stage(st + 1, cur ^ 1);
         __syncthreads();
-        if (threadIdx.x < kMStage && t0 + threadIdx.x < nt && colmin[threadIdx.x] != 0x7FFFFFFF)
-            atomicMin(&bwd[t0 + threadIdx.x], colmin[threadIdx.x]);
+        const int t = st * kMStage + threadIdx.x;
+        if (threadIdx.x < kMStage && t < nt && colmin[cur][threadIdx.x] != 0x7FFFFFFF)
+            atomicMin(&bwd[t], key_old(colmin[cur][threadIdx.x]));
     }
     // forward: minimum over the 32 lanes of each half (they hold the 32 columns)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-            int v = best[s2][g];
+            int vv = best[s2][g];
 #pragma unroll
-            for (int o = 1; o < 32; o <<= 1) v = min(v, __shfl_xor(v, o));
+            for (int o = 1; o < 32; o <<= 1) vv = min(vv, __shfl_xor(vv, o));
             const int qr = qs + 32 * s2 + (g & 3) + 8 * (g >> 2) + 4 * h;
-            if (r == g && qr < nq) fwd[qr] = nt > 0 ? v : -1;
+            if (r == g && qr < nq) fwd[qr] = nt > 0 ? key_old(vv) : -1;
         }
 }
 
@@ -451,7 +480,9 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     // backward keys start at 0x7F7F7F7F ("none") and are lowered by atomicMin
     hipError_t e = hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F, sizeof(int32_t) * (size_t)P.nframes * cap, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(nn_mfma_kernel, dim3((cap + kMQB - 1) / kMQB, P.nframes - 1), dim3(256), 0, s, P);
+    const int pairs = P.nframes - 1, nqb = (cap + kMQB - 1) / kMQB;
+    const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();
