@@ -226,12 +226,14 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
             acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1][ks], B, acc1, 0, 0, 0);
         }
         int cm = 0x7FFFFFFF;
+        int rb = rowb;
+        asm volatile("" : "+v"(rb));  // keep rowb + goff out of 32 hoisted registers: one v_add3 per element
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int goff = (g & 3) + 8 * (g >> 2);
             best[0][g] = min(best[0][g], acc0[g] + cf);
             best[1][g] = min(best[1][g], acc1[g] + cf);
-            int k0 = acc0[g] + (rowb + goff), k1 = acc1[g] + (rowb + 32 + goff);
+            int k0 = acc0[g] + rb + goff, k1 = acc1[g] + rb + (32 + goff);
             if (!kFull) {
                 k0 = rowb - kKeyBase + goff < nq ? k0 : kKeyNone;
                 k1 = rowb - kKeyBase + 32 + goff < nq ? k1 : kKeyNone;
