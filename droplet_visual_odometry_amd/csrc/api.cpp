@@ -109,7 +109,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         // x table padded to a multiple of 4 entries at a 16-byte aligned offset (one int4 per 4 columns)
         G.xcoef_off = l == 0 ? 0 : coef;
         G.ycoef_off = l == 0 ? 0 : coef + ((G.w + 3) & ~3);
-        if (l > 0) coef += ((G.w + 3) & ~3) + ((G.h + 3) & ~3);  // y table padded the same way
+        if (l > 0) coef += ((G.w + 3) & ~3) + ((G.h + 7) & ~7);  // y table padded to 8 rows (resize_level_lds_kernel)
         const bool usable = G.w > 2 * kBorder && G.h > 2 * kBorder;
         const int rows = usable ? G.h - 2 * kBorder : 0;
         const int wc = usable ? G.w - 2 * kBorder : 0;
@@ -167,7 +167,7 @@ std::vector<int32_t> resize_coefs(const Plan& p) {
     for (int l = 1; l < p.nlevels; ++l) {
         const LevelGeom &S = p.L[l - 1], &D = p.L[l];
         for (int x = 0; x < ((D.w + 3) & ~3); ++x) c[D.xcoef_off + x] = lin_coef_packed(std::min(x, D.w - 1), S.w, D.w);
-        for (int y = 0; y < ((D.h + 3) & ~3); ++y) c[D.ycoef_off + y] = lin_coef_packed(std::min(y, D.h - 1), S.h, D.h);
+        for (int y = 0; y < ((D.h + 7) & ~7); ++y) c[D.ycoef_off + y] = lin_coef_packed(std::min(y, D.h - 1), S.h, D.h);
     }
     return c;
 }

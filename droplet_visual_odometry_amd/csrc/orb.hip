@@ -131,14 +131,15 @@ __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l
 }
 
 // LDS-staged variant for level ratios <= 1.25 (ORB's 1.2 pyramid): the
-// workgroup's output tile (256 columns x 16 rows) needs at most kRsW source
+// workgroup's output tile (256 columns x 32 rows) needs at most kRsW source
 // words x kRsRows source rows; each wave stages whole source rows with
 // coalesced word loads (lane k <- word k), then every lane reads its 3 words
 // per source row from LDS.  Same arithmetic as resize_level_kernel.
-constexpr int kRsW = 96, kRsRows = 24;
+constexpr int kRsLR = 8;  // output rows per wave (32 per workgroup)
+constexpr int kRsW = 96, kRsLRows = 44;  // 32 * 1.25 + 2 source rows, padded to a multiple of 4
 
 __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l) {
-    __shared__ uint32_t tile[kRsRows][kRsW];
+    __shared__ uint32_t tile[kRsLRows][kRsW];
     const int f = blockIdx.z;
     const LevelGeom& S = P.plan.L[l - 1];
     const LevelGeom& D = P.plan.L[l];
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int xa = blockIdx.x * 256;
     const int x0 = xa + 4 * lane;
-    const int ty0 = blockIdx.y * (4 * kRsR);
+    const int ty0 = blockIdx.y * (4 * kRsLR);
     const uint8_t* src = level_ptr(P, f, l - 1);
     const int sp = level_pitch(P, l - 1);
     uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
@@ -156,29 +157,32 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int sx0 = coef_ofs(cxt[xa]) & ~3;
     const int nw = ((coef_ofs(cxt[min(xa + 255, D.w - 1)]) + 1 - sx0) >> 2) + 1;
     const int sy0 = coef_ofs(cyt[ty0]);
-    const int nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
+    const int nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsLR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
     // this lane's taps (issued before the staging so their latency overlaps it)
     const int4 cx = *reinterpret_cast<const int4*>(cxt + min(x0, ((D.w + 3) & ~3) - 4));
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
-    {  // kRsRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
-        uint32_t v0[kRsRows / 4], v1[kRsRows / 4];
+    {  // kRsLRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
+        uint32_t v0[kRsLRows / 4], v1[kRsLRows / 4];
 #pragma unroll
-        for (int it = 0; it < kRsRows / 4; ++it) {
+        for (int it = 0; it < kRsLRows / 4; ++it) {
             const int soff = (sy0 + min(wid + 4 * it, nr - 1)) * sp;
             v0[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane, soff, 0);
             v1[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane + 256, soff, 0);
         }
 #pragma unroll
-        for (int it = 0; it < kRsRows / 4; ++it) {
+        for (int it = 0; it < kRsLRows / 4; ++it) {
             tile[wid + 4 * it][lane] = v0[it];
             if (lane + 64 < kRsW) tile[wid + 4 * it][lane + 64] = v1[it];
         }
     }
     __syncthreads();
-    const int dy0 = ty0 + wid * kRsR;
+    const int dy0 = ty0 + wid * kRsLR;
     if (dy0 >= D.h) return;
-    const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform
-    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w}, cys[4] = {cy.x, cy.y, cy.z, cy.w};
+    const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform (table padded to 8 rows)
+    const int4 cz = *reinterpret_cast<const int4*>(cyt + dy0 + 4);
+    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w};
+    const int cys[kRsLR] = {cy.x, cy.y, cy.z, cy.w, cz.x, cz.y, cz.z, cz.w};
+    static_assert(kRsLR == 8, "two int4 row-coefficient loads");
     int i0[4], c1[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -189,12 +193,12 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int base = 4 * wb0;
     const bool full = x0 + 4 <= D.w;
 #pragma unroll
-    for (int rr = 0; rr < kRsR; ++rr) {
+    for (int rr = 0; rr < kRsLR; ++rr) {
         const int dy = dy0 + rr;
         if (dy >= D.h) break;
         const int lr = coef_ofs(cys[rr]) - sy0;
         const uint32_t cy1 = coef_c1(cys[rr]);
-        const int lr1 = min(lr + 1, kRsRows - 1);  // weight-0 row past the window: any in-range row
+        const int lr1 = min(lr + 1, kRsLRows - 1);  // weight-0 row past the window: any in-range row
         const uint32_t wa[3] = {tile[lr][wb0], tile[lr][wb0 + 1], tile[lr][wb0 + 2]};
         const uint32_t wb[3] = {tile[lr1][wb0], tile[lr1][wb0 + 1], tile[lr1][wb0 + 2]};
         uint32_t word = 0;
@@ -1300,14 +1304,16 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const int F = P.nframes;
     mark(ev, 0, 0, s);
     for (int l = 1; l < pl.nlevels; ++l) {
-        dim3 grid((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsR - 1) / (4 * kRsR), F);
         // staged tile fits when both ratios are <= 1.25: 256 * 1.25 + 12 bytes <= kRsW words,
-        // 16 * 1.25 + 2 rows <= kRsRows
+        // 32 * 1.25 + 2 rows <= kRsRows
         const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
         if (lds)
-            hipLaunchKernelGGL(resize_level_lds_kernel, grid, dim3(256), 0, s, P, l);
+            hipLaunchKernelGGL(resize_level_lds_kernel,
+                               dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR), F), dim3(256), 0,
+                               s, P, l);
         else
-            hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P, l);
+            hipLaunchKernelGGL(resize_level_kernel, dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsR - 1) / (4 * kRsR), F),
+                               dim3(256), 0, s, P, l);
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
