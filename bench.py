@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+PMC_TRAFFIC = "r01c_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
 
 
 def parse():
@@ -287,9 +288,9 @@ def chained_ate(fs, pool, corners, K, ref, B):
 
 def pmc_traffic(kernel, W, H, N, B):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/r01_pmc_traffic.json: FETCH_SIZE + WRITE_SIZE), when they were
+    (profiles/PMC_TRAFFIC: FETCH_SIZE + WRITE_SIZE), when they were
     taken on this configuration; PMC counters cannot run inside the timed loop."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
     try:
         doc = json.load(open(path))
     except (OSError, ValueError):
@@ -298,7 +299,7 @@ def pmc_traffic(kernel, W, H, N, B):
     k = doc.get("kernels", {}).get(kernel)
     if k is None or (c.get("width"), c.get("height"), c.get("nfeatures"), c.get("batch")) != (W, H, N, B):
         return None, None
-    return round(k["fetch_bytes"] + k["write_bytes"]), "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"
+    return round(k["fetch_bytes"] + k["write_bytes"]), f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"
 
 
 def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
