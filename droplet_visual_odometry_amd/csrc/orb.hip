@@ -502,7 +502,8 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
     __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+20)
     __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+17)
-    __shared__ uint16_t cand[4 * kFtSeg], corner[4 * kFtSeg];
+    // + 64 slots per wave that lanes without an entry store to (branch-free appends: no exec-mask SALU)
+    __shared__ uint16_t cand[4 * kFtSeg + 256], corner[4 * kFtSeg + 256];
     __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
     __shared__ int ncand[4], ncorner[4], ncarry[2];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
@@ -574,7 +575,8 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         const int nsr = nrows + 2;
         const int sr_lo = b == 0 ? 0 : 2;
         {
-            uint16_t* seg = cand + wid * kFtSeg;
+            const int seg_off = wid * kFtSeg, spare_i = 4 * kFtSeg + wid * 64 + lane;
+            const uint32_t okm = (ok0 ? 1u : 0u) | (ok1 ? 2u : 0u);
             int n = 0;  // wave-uniform
             for (int sr = sr_lo + ((wid - sr_lo) & 3); sr < nsr; sr += kFastNT / 64) {
                 const int a = (sr + 3) * kFtLW + (x_lo - bx);
@@ -583,25 +585,19 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
                     const int ah = a + 64 * hh;
                     const int v = img[ah];
                     const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
-#if defined(FAST_EXP) && FAST_EXP == 2
-                    const bool pass = (hh ? ok1 : ok0) & (v > 1000);
-#else
-                    const bool pass = (hh ? ok1 : ok0) &
-                                      ((min(max(c0, c8), max(c4, c12)) > v + thr) | (max(min(c0, c8), min(c4, c12)) < v - thr));
-#endif
-                    const unsigned long long bal = __ballot(pass);
-                    if (pass) seg[n + lane_prefix(bal)] = (uint16_t)ah;
+                    // the whole condition as integer arithmetic (sign bits: no compare masks, no exec
+                    // changes), one compare for the ballot, the store address selected arithmetically
+                    const int X = min(max(c0, c8), max(c4, c12)), Y = max(min(c0, c8), min(c4, c12));
+                    const uint32_t pm = ((uint32_t)((v + thr - X) | (Y - v + thr)) >> 31) & (okm >> hh);
+                    const unsigned long long bal = __ballot(pm != 0);
+                    const int to = seg_off + n + (int)lane_prefix(bal);
+                    cand[spare_i + __mul24((int)pm, to - spare_i)] = (uint16_t)ah;
                     n += __popcll(bal);
                 }
             }
             if (lane == 0) ncand[wid] = n;
         }
         __syncthreads();
-#if defined(FAST_EXP) && FAST_EXP == 1
-        if (wid == 0 && lane < kBandRows) P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = 0;
-        __syncthreads();
-        continue;
-#endif
         // ---- segment test over the concatenated candidates, corners into this wave's corner segment
         {
             int cnt[4];
@@ -609,6 +605,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
             const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
             uint16_t* seg = corner + wid * kFtSeg;
+            uint16_t* const spare = corner + 4 * kFtSeg + wid * 64 + lane;
             int n = 0;
             for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
                 const int e = e0 + lane;
@@ -629,17 +626,12 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
                     is_corner = has_run9(br) || has_run9(dk);
                 }
                 const unsigned long long bal = __ballot(is_corner);
-                if (is_corner) seg[n + lane_prefix(bal)] = (uint16_t)a;
+                *(is_corner ? seg + n + lane_prefix(bal) : spare) = (uint16_t)a;
                 n += __popcll(bal);
             }
             if (lane == 0) ncorner[wid] = n;
         }
         __syncthreads();
-#if defined(FAST_EXP) && FAST_EXP == 3
-        if (wid == 0 && lane < kBandRows) P.buf.band_cnt[((int64_t)f * P.plan.total_bands + item) * kBandRows + lane] = 0;
-        __syncthreads();
-        continue;
-#endif
         int cnt2[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cnt2[k] = ncorner[k];
