@@ -17,6 +17,7 @@
 #include "dvo_internal.h"
 
 #include <climits>
+#include <type_traits>
 
 namespace dvo {
 
@@ -578,23 +579,30 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             const int seg_off = wid * kFtSeg, spare_i = 4 * kFtSeg + wid * 64 + lane;
             const uint32_t okm = (ok0 ? 1u : 0u) | (ok1 ? 2u : 0u);
             int n = 0;  // wave-uniform
-            for (int sr = sr_lo + ((wid - sr_lo) & 3); sr < nsr; sr += kFastNT / 64) {
-                const int a = (sr + 3) * kFtLW + (x_lo - bx);
+            // interior strips (every score column valid) skip the column mask
+            auto rows = [&](auto interior) {
+                for (int sr = sr_lo + ((wid - sr_lo) & 3); sr < nsr; sr += kFastNT / 64) {
+                    const int a = (sr + 3) * kFtLW + (x_lo - bx);
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int ah = a + 64 * hh;
-                    const int v = img[ah];
-                    const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
-                    // the whole condition as integer arithmetic (sign bits: no compare masks, no exec
-                    // changes), one compare for the ballot, the store address selected arithmetically
-                    const int X = min(max(c0, c8), max(c4, c12)), Y = max(min(c0, c8), min(c4, c12));
-                    const uint32_t pm = ((uint32_t)((v + thr - X) | (Y - v + thr)) >> 31) & (okm >> hh);
-                    const unsigned long long bal = __ballot(pm != 0);
-                    const int to = seg_off + n + (int)lane_prefix(bal);
-                    cand[spare_i + __mul24((int)pm, to - spare_i)] = (uint16_t)ah;
-                    n += __popcll(bal);
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const int ah = a + 64 * hh;
+                        const int v = img[ah];
+                        const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
+                        // the whole condition as integer arithmetic: max(X - v, v - Y) > t from a sign bit
+                        // (no compare masks, no exec changes); one compare for the ballot; the store
+                        // address selected (lanes that do not pass write their spare slot)
+                        const int X = min(max(c0, c8), max(c4, c12)), Y = max(min(c0, c8), min(c4, c12));
+                        uint32_t pm = (uint32_t)(thr - max(X - v, v - Y)) >> 31;
+                        if (!decltype(interior)::value) pm &= okm >> hh;
+                        const unsigned long long bal = __ballot(pm != 0);
+                        const int to = seg_off + n + (int)lane_prefix(bal);
+                        cand[pm ? to : spare_i] = (uint16_t)ah;
+                        n += __popcll(bal);
+                    }
                 }
-            }
+            };
+            if (__ballot(okm != 3) == 0) rows(std::true_type{});  // wave-uniform choice
+            else rows(std::false_type{});
             if (lane == 0) ncand[wid] = n;
         }
         __syncthreads();
