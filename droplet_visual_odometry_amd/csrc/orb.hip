@@ -1116,7 +1116,10 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // blurred 39 x 44 window around it (word loads into LDS); the 512 rBRIEF
 // samples are then LDS reads.
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
-constexpr int kDKW = 1;                // keypoints per wave
+#ifndef DVO_DKW
+#define DVO_DKW 1
+#endif
+constexpr int kDKW = DVO_DKW;          // keypoints per wave
 constexpr int kDKB = 4 * kDKW;         // keypoints per workgroup
 constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padding) x 9 aligned words
 

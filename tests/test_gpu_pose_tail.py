@@ -83,3 +83,35 @@ def test_two_streams_share_one_pose_chain(gpu_ctx):
         np.testing.assert_array_equal(g.cpu().numpy(), w.cpu().numpy())
     for fs in (ref, a, b):
         fs.close()
+
+
+def test_pose_tail_from_stag_messages(gpu_ctx, oracle_mod):
+    """Corners arriving as StagMarkers-style messages (traj_eval_ground_truth.py:303-311),
+    packed by marker_corner_batch, drive the same device tail as raw arrays."""
+    import os
+    import sys
+    from types import SimpleNamespace as NS
+    import torch
+    from conftest import ROOT, synth_frames
+    sys.path.insert(0, os.path.join(ROOT, "droplet_visual_odometry_amd", "dropin"))
+    import marker_corners as mc
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    frames, K = synth_frames(640, 480, range(4))
+    corners = [marker_corners(i, K) for i in range(4)]
+    msgs = [NS(markers=[NS(id=0, corners=[NS(x=x, y=y) for x, y in c])]) for c in corners]
+    dc = mc.marker_corner_batch(msgs, device="cuda")
+    fs = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    fs.reset_pose()
+    rec = fs.process(torch.from_numpy(frames).cuda())
+    T_rel, T_abs = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
+    fs.sync()
+    recs = FrameStream.records_numpy(rec, 3)
+    P, T = K @ np.hstack((np.eye(3), np.zeros((3, 1)))), np.eye(4)
+    T_abs = T_abs.cpu().numpy()
+    for p in range(3):
+        assert recs[p]["status"] == 0
+        P, _, T = oracle_mod.pose_tail(K, recs[p]["R"].reshape(3, 3), recs[p]["t"], corners[p], corners[p + 1],
+                                       MARKER_LEN, P, T)
+        np.testing.assert_allclose(T_abs[p], T, rtol=1e-9, atol=1e-12)
+    fs.close()
