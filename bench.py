@@ -32,7 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-PMC_TRAFFIC = "r01c_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
+PMC_TRAFFIC = "r01d_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
 
 
 def parse():
@@ -297,9 +297,13 @@ def pmc_traffic(kernel, W, H, N, B):
         return None, None
     c = doc.get("config", {})
     k = doc.get("kernels", {}).get(kernel)
-    if k is None or (c.get("width"), c.get("height"), c.get("nfeatures"), c.get("batch")) != (W, H, N, B):
+    if k is None or (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
         return None, None
-    return round(k["fetch_bytes"] + k["write_bytes"]), f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"
+    # one launch covers B + 1 frames: the counted bytes scale per frame from the profiled batch
+    scale = (B + 1) / (c["batch"] + 1)
+    src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE at batch {c['batch']}"
+    src += ")" if c["batch"] == B else f", scaled per frame to batch {B})"
+    return round((k["fetch_bytes"] + k["write_bytes"]) * scale), src
 
 
 def cpu_baseline(pool, K, nfeatures, max_iters, seconds):

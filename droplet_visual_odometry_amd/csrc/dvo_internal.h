@@ -19,7 +19,10 @@ constexpr int kBandRows = 16;       // FAST tile height (output rows)
 constexpr int kFastTW = 126;        // FAST tile width (output columns; score window 128)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
-constexpr int kBlurTW = 248, kBlurTH = 64;  // blur tile: 62 lanes x 4 columns, 4 waves x 16 rows
+#ifndef DVO_BLUR_TH
+#define DVO_BLUR_TH 96
+#endif
+constexpr int kBlurTW = 248, kBlurTH = DVO_BLUR_TH;  // blur tile: 62 lanes x 4 columns, 4 waves x kBlurTH / 4 rows
 
 // Per-level geometry of one ORB plan (identical for every frame of a stream).
 struct LevelGeom {
