@@ -1004,7 +1004,10 @@ __global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
 // [0, min(256, niters)) and round 2 everything left, [256, niters): the result
 // is the sequential loop's, bit for bit.
 constexpr int kSolveNT = 64;
-constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = 1024;
+#ifndef DVO_SCORE_CHUNK
+#define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
+#endif
+constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 
 __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round) {
     const int p = blockIdx.x * 64 + threadIdx.x;
