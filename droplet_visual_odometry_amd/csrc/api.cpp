@@ -687,6 +687,42 @@ int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t*
     return DVO_OK;
 }
 
+int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
+                     int32_t* train_idx, float* dist) {
+    if (!ctx) return DVO_EINVAL;
+    if (norm != DVO_NORM_L1 && norm != DVO_NORM_L2SQR) return fail(ctx, DVO_EINVAL, "norm must be DVO_NORM_L1 or DVO_NORM_L2SQR");
+    if (dim != 64 && dim != 128) return fail(ctx, DVO_EINVAL, "descriptor length must be 64 (SURF) or 128 (SIFT)");
+    if (k < 1 || k > 4) return fail(ctx, DVO_EINVAL, "k must be 1..4");
+    if (nq < 0 || nt < 0 || nq > (1 << 20) || nt > (1 << 20))
+        return fail(ctx, DVO_EINVAL, "descriptor count out of range (0..2^20)");
+    if (nq == 0) return DVO_OK;
+    if (!dq || !train_idx || !dist || (nt > 0 && !dt)) return fail(ctx, DVO_EINVAL, "null buffer");
+    if (nt == 0) {  // batchDistance leaves every slot at (-1, FLT_MAX)
+        for (size_t i = 0; i < (size_t)nq * k; ++i) {
+            train_idx[i] = -1;
+            dist[i] = FLT_MAX;
+        }
+        return DVO_OK;
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int chunks = knn_chunks(nt);
+    const size_t out_n = (size_t)nq * k, part_n = chunks > 1 ? (size_t)chunks * nq * k : 1;
+    void *bq, *bt, *bd, *bi, *bpd, *bpi;
+    int rc;
+    if ((rc = scratch(ctx, 27, (size_t)nq * dim * 4, &bq)) || (rc = scratch(ctx, 28, (size_t)nt * dim * 4, &bt)) ||
+        (rc = scratch(ctx, 29, out_n * 4, &bd)) || (rc = scratch(ctx, 30, out_n * 4, &bi)) ||
+        (rc = scratch(ctx, 31, part_n * 4, &bpd)) || (rc = scratch(ctx, 32, part_n * 4, &bpi)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(bq, dq, (size_t)nq * dim * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(bt, dt, (size_t)nt * dim * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_knn_float((const float*)bq, nq, (const float*)bt, nt, dim, k, norm, (float*)bpd, (int32_t*)bpi,
+                             (float*)bd, (int32_t*)bi, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dist, bd, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(train_idx, bi, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return DVO_OK;
+}
+
 static int upload_points(dvo_ctx* ctx, const double* p1, const double* p2, int m, void** dpts) {
     int rc = scratch(ctx, 5, (size_t)(m > 0 ? m : 1) * 32, dpts);
     if (rc) return rc;

@@ -14,6 +14,8 @@
 // directions run in the same launch (grid.y).
 // crosscheck_sort_kernel: mutual-NN filter, then a bitonic sort of the unique
 // keys (distance << 16 | queryIdx) in LDS, then the point gather.
+#include <cfloat>
+
 #include "dvo_internal.h"
 
 namespace dvo {
@@ -498,6 +500,158 @@ hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int
     hipLaunchKernelGGL(nn_pair_kernel, grid, dim3(kNNThreads), lds, s, d_q, nq, d_t, nt, d_nn);
     hipLaunchKernelGGL(crosscheck_pair_kernel, dim3(1), dim3(kXNT), 0, s, d_nn, nq, nt, cross_check, d_out, d_m);
     return hipGetLastError();
+}
+
+// ---- float descriptors: BFMatcher(NORM_L1).knnMatch / FLANN stand-in ---------
+// The SIFT/SURF branches (visual_odometry_v3.py:99-106, :200-215).  One thread
+// per query holds its descriptor in registers; a workgroup scans a chunk of
+// kKnnTC trains whose rows are wave-uniform, so they arrive through scalar
+// loads (SGPR operands of the VALU ops, no LDS or per-lane traffic).  Grid:
+// x = query blocks, y = train chunks; each (query, chunk) keeps its K best in
+// OpenCV's batchDistance order (enter iff d < dist[K-1], land after entries
+// with dist <= d), and a merge kernel folds the chunks in train order, which
+// reproduces the sequential scan exactly (oracle ora_bf_knn_float).
+namespace {
+
+constexpr int kKnnQ = 256;  // queries per workgroup (one per thread)
+constexpr int kKnnTC = 64;  // trains per workgroup
+
+template <int D, int NORM>
+__device__ __forceinline__ float desc_distance(const float (&q)[D], const float* __restrict__ t) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; i += 4) {
+        const float d0 = q[i] - t[i], d1 = q[i + 1] - t[i + 1], d2 = q[i + 2] - t[i + 2], d3 = q[i + 3] - t[i + 3];
+        if constexpr (NORM == 0) {
+            s += ((fabsf(d0) + fabsf(d1)) + fabsf(d2)) + fabsf(d3);  // cv::normL1 (base.hpp)
+        } else {
+            s += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;  // flann::L2 (no contraction: -ffp-contract=off)
+        }
+    }
+    return s;
+}
+
+template <int K>
+__device__ __forceinline__ void knn_insert(float (&bd)[K], int (&bi)[K], float d, int j) {
+    if (!(d < bd[K - 1])) return;
+#pragma unroll
+    for (int s = K - 1; s >= 0; --s) {
+        // sorted ascending: slot s keeps its entry if <= d, else takes d (when
+        // slot s-1 is <= d) or the entry shifted down from s-1
+        if (bd[s] > d) {
+            if (s > 0 && bd[s - 1] > d) {
+                bd[s] = bd[s - 1];
+                bi[s] = bi[s - 1];
+            } else {
+                bd[s] = d;
+                bi[s] = j;
+            }
+        }
+    }
+}
+
+template <int D, int NORM, int K>
+__global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restrict__ q, int nq,
+                                                          const float* __restrict__ t, int nt,
+                                                          float* __restrict__ odist, int32_t* __restrict__ oidx) {
+    const int qi = blockIdx.x * kKnnQ + threadIdx.x;
+    const int qs = qi < nq ? qi : nq - 1;  // clamped: spare lanes compute, never store
+    float qv[D];
+    const float4* q4 = reinterpret_cast<const float4*>(q + (size_t)qs * D);
+#pragma unroll
+    for (int i = 0; i < D / 4; ++i) {
+        const float4 v = q4[i];
+        qv[4 * i] = v.x;
+        qv[4 * i + 1] = v.y;
+        qv[4 * i + 2] = v.z;
+        qv[4 * i + 3] = v.w;
+    }
+    float bd[K];
+    int bi[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        bd[s] = FLT_MAX;
+        bi[s] = -1;
+    }
+    const int j0 = blockIdx.y * kKnnTC, j1 = min(nt, j0 + kKnnTC);
+    for (int j = j0; j < j1; ++j) knn_insert<K>(bd, bi, desc_distance<D, NORM>(qv, t + (size_t)j * D), j);
+    if (qi < nq) {
+        const size_t o = ((size_t)blockIdx.y * nq + qi) * K;
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            odist[o + s] = bd[s];
+            oidx[o + s] = bi[s];
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
+                                                        int nq, int chunks, float* __restrict__ odist,
+                                                        int32_t* __restrict__ oidx) {
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (qi >= nq) return;
+    float bd[K];
+    int bi[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        bd[s] = FLT_MAX;
+        bi[s] = -1;
+    }
+    for (int c = 0; c < chunks; ++c) {
+        const size_t o = ((size_t)c * nq + qi) * K;
+#pragma unroll
+        for (int s = 0; s < K; ++s)
+            if (pidx[o + s] >= 0) knn_insert<K>(bd, bi, pdist[o + s], pidx[o + s]);
+    }
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        odist[(size_t)qi * K + s] = bd[s];
+        oidx[(size_t)qi * K + s] = bi[s];
+    }
+}
+
+template <int D, int NORM, int K>
+hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, float* d_part, int32_t* d_pidx,
+                        float* d_dist, int32_t* d_idx, hipStream_t s) {
+    const int chunks = (nt + kKnnTC - 1) / kKnnTC;
+    const dim3 grid((nq + kKnnQ - 1) / kKnnQ, chunks);
+    if (chunks == 1) {
+        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, d_dist, d_idx);
+    } else {
+        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, d_part, d_pidx);
+        hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 255) / 256), dim3(256), 0, s, d_part, d_pidx, nq, chunks,
+                           d_dist, d_idx);
+    }
+    return hipGetLastError();
+}
+
+template <int D, int NORM>
+hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int nt, float* d_part, int32_t* d_pidx,
+                        float* d_dist, int32_t* d_idx, hipStream_t s) {
+    switch (k) {
+        case 1: return launch_knn_t<D, NORM, 1>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        case 2: return launch_knn_t<D, NORM, 2>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        case 3: return launch_knn_t<D, NORM, 3>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        case 4: return launch_knn_t<D, NORM, 4>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+int knn_chunks(int nt) { return (nt + kKnnTC - 1) / kKnnTC; }
+
+hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm,
+                            float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
+    if (nq <= 0 || nt <= 0) return hipSuccess;
+    if (dim == 128)
+        return norm == 0 ? launch_knn_k<128, 0>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<128, 1>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+    if (dim == 64)
+        return norm == 0 ? launch_knn_k<64, 0>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<64, 1>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace dvo

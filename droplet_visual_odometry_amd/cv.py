@@ -3,6 +3,9 @@
 The reference calls (scripts/visual_odometry_v3.py):
   cv.ORB_create()                                       :96
   cv.BFMatcher(normType=NORM_HAMMING, crossCheck=True)  :75    .match :219
+  cv.BFMatcher(normType=NORM_L1) .match / .knnMatch(k=2) :99-106, :200-204, :214-215 (SIFT/SURF)
+  cv.FlannBasedMatcher(index, search).knnMatch(k=2)     :206-212 (exact-search stand-in)
+  cv.xfeatures2d.SIFT_create() / SURF_create(400)       :100, :104 (host cv2 when importable)
   detector.detectAndCompute(img, None)                  :373
   cv.drawKeypoints(img, kps, None, color, flags=0)      :375   (result discarded, D6)
   cv.KeyPoint_convert(kps)                              :355, :358
@@ -140,24 +143,61 @@ def ORB_create(nfeatures=500, scaleFactor=1.2, nlevels=8, edgeThreshold=31, firs
     return ORB(nfeatures, scaleFactor, nlevels, edgeThreshold, firstLevel, WTA_K, scoreType, patchSize, fastThreshold)
 
 
+def _float_desc(d):
+    a = np.asarray(d)
+    if a.ndim != 2 or a.dtype != np.float32:
+        raise error("(-215:Assertion failed) NORM_L1 / FLANN matching needs float32 [N, dim] descriptors")
+    return a
+
+
+def _knn_lists(q, t, k, norm):
+    if len(q) == 0 or len(t) == 0:
+        return [[] for _ in range(len(q))] if len(t) == 0 else []
+    if q.shape[1] != t.shape[1]:
+        raise error("(-215:Assertion failed) query and train descriptors differ in length")
+    try:
+        idx, dist = ops.bf_knn_float(q, t, k, norm)
+    except DVOError as e:
+        raise error(str(e)) from e
+    out = []
+    for qi in range(len(q)):
+        row = []
+        for s in range(k):
+            if idx[qi, s] < 0:
+                break
+            row.append(DMatch(qi, int(idx[qi, s]), 0, float(dist[qi, s])))
+        out.append(row)
+    return out
+
+
 class BFMatcher:
-    """cv2.BFMatcher; NORM_HAMMING only (the ORB branch, v3:75, v3:97).
+    """cv2.BFMatcher: NORM_HAMMING (the ORB branch, v3:75, v3:97) and NORM_L1
+    on float descriptors (the SIFT/SURF branches, v3:99-106).
 
     crossCheck follows OpenCV 4.x (mutual nearest neighbour) unless
-    legacy_crosscheck=True selects OpenCV 3.x's reverse-pass semantics."""
+    legacy_crosscheck=True selects OpenCV 3.x's reverse-pass semantics; it is
+    implemented for NORM_HAMMING (the reference sets it only there)."""
 
     def __init__(self, normType=NORM_L2, crossCheck=False, legacy_crosscheck=False):
         self.normType = normType
         self.crossCheck = bool(crossCheck)
         self.legacy_crosscheck = bool(legacy_crosscheck)
 
+    def _check_l1(self):
+        if self.normType != NORM_L1:
+            raise error("only NORM_HAMMING (ORB) and NORM_L1 (SIFT/SURF) are implemented on the GPU")
+        if self.crossCheck:
+            raise error("crossCheck is implemented for NORM_HAMMING only (the reference's L1 modes pass False)")
+
     def match(self, queryDescriptors, trainDescriptors, mask=None):
         if mask is not None:
             raise error("match masks are not supported")
         if queryDescriptors is None or trainDescriptors is None:
             raise error("(-215:Assertion failed) descriptors must not be empty")
-        if self.normType not in (NORM_HAMMING,):
-            raise error("only NORM_HAMMING (ORB) is implemented on the GPU; SIFT/SURF/FLANN modes are §8f 'next'")
+        if self.normType != NORM_HAMMING:
+            self._check_l1()
+            return [row[0] for row in _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), 1,
+                                                 ops.NORM_L1) if row]
         q = np.asarray(queryDescriptors)
         t = np.asarray(trainDescriptors)
         if q.dtype != np.uint8 or t.dtype != np.uint8 or q.shape[-1] != 32 or t.shape[-1] != 32:
@@ -169,8 +209,34 @@ class BFMatcher:
             raise error(str(e)) from e
         return [DMatch(int(a), int(b), 0, float(d)) for a, b, d in zip(m["queryIdx"], m["trainIdx"], m["distance"])]
 
-    def knnMatch(self, *a, **k):
-        raise error("knnMatch (SIFT/SURF/knn_sift modes) is outside the ORB hot path (SURVEY.md §8f rank 4)")
+    def knnMatch(self, queryDescriptors, trainDescriptors, k, mask=None, compactResult=False):
+        """List (one per query) of up to k DMatch in ascending distance."""
+        if mask is not None:
+            raise error("match masks are not supported")
+        if queryDescriptors is None or trainDescriptors is None:
+            raise error("(-215:Assertion failed) descriptors must not be empty")
+        self._check_l1()
+        out = _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), int(k), ops.NORM_L1)
+        return [r for r in out if r] if compactResult else out
+
+
+class FlannBasedMatcher:
+    """cv2.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50)) as
+    built at v3:206-212.  Served by EXACT k-nearest-neighbour search in FLANN's
+    distance (squared L2): FLANN's randomized kd-trees return the same
+    neighbours whenever their approximate search finds the true ones; where it
+    misses (seed dependent in OpenCV) the results differ — a documented
+    deviation (DESIGN.md row f)."""
+
+    def __init__(self, indexParams=None, searchParams=None):
+        self.indexParams = dict(indexParams or {})
+        self.searchParams = dict(searchParams or {})
+
+    def knnMatch(self, queryDescriptors, trainDescriptors, k, mask=None, compactResult=False):
+        if mask is not None:
+            raise error("match masks are not supported")
+        out = _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), int(k), ops.NORM_L2SQR)
+        return [r for r in out if r] if compactResult else out
 
 
 def findEssentialMat(points1, points2, cameraMatrix=None, method=RANSAC, prob=0.999, threshold=1.0, maxIters=1000,
@@ -336,14 +402,33 @@ def drawKeypoints(image, keypoints, outImage=None, color=(0, 255, 0), flags=0):
     return out
 
 
+def _host_cv2():
+    try:
+        import cv2  # noqa: F401  (detection only; matching stays on the GPU)
+        return cv2
+    except ImportError:
+        return None
+
+
 class _XFeatures2d:
+    """SIFT / SURF detection (v3:100, :104) is CPU work in the reference and is
+    not on the accelerated path: these return the host cv2 detector when cv2
+    is importable (its descriptors then feed the GPU matchers above) and
+    raise cv.error otherwise."""
+
     @staticmethod
     def SIFT_create(*a, **k):
-        raise error("SIFT is outside the ORB hot path (SURVEY.md §8f rank 4)")
+        cv2 = _host_cv2()
+        if cv2 is None:
+            raise error("SIFT detection needs the host cv2 package (not installed); matching is on the GPU")
+        return cv2.SIFT_create(*a, **k) if hasattr(cv2, "SIFT_create") else cv2.xfeatures2d.SIFT_create(*a, **k)
 
     @staticmethod
     def SURF_create(*a, **k):
-        raise error("SURF is outside the ORB hot path (SURVEY.md §8f rank 4)")
+        cv2 = _host_cv2()
+        if cv2 is None or not hasattr(cv2, "xfeatures2d"):
+            raise error("SURF detection needs the host cv2 contrib package (not installed); matching is on the GPU")
+        return cv2.xfeatures2d.SURF_create(*a, **k)
 
 
 xfeatures2d = _XFeatures2d()

@@ -168,7 +168,8 @@ class VisualOdometry:
         elif self.mode in ("knn_sift", "surf"):
             matches = self.bf.knnMatch(previous_descriptors, current_descriptors, k=2)
         elif self.mode == "flann":
-            raise cv.error("FLANN matching is outside the ORB hot path (SURVEY.md §8f rank 4)")
+            flann = cv.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50))
+            matches = flann.knnMatch(previous_descriptors, current_descriptors, k=2)
         elif self.mode == "orb":
             matches = sorted(self.bf.match(previous_descriptors, current_descriptors), key=lambda x: x.distance)
         if self.mode != "orb":

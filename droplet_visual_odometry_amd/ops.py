@@ -5,6 +5,8 @@ mirrors its argument meaning, output layout and failure points:
 
   detect_and_compute   cv::ORB::detectAndCompute          visual_odometry_v3.py:373
   bf_match             cv::BFMatcher(NORM_HAMMING).match  visual_odometry_v3.py:75, :219
+  bf_knn_float         cv::BFMatcher(NORM_L1).knnMatch / .match, FLANN knnMatch
+                                                          visual_odometry_v3.py:99-106, :200-215
   find_essential_mat   cv::findEssentialMat(RANSAC)       visual_odometry_v3.py:297-300
   recover_pose         cv::recoverPose                    visual_odometry_v3.py:303-306
   triangulate_points   cv::triangulatePoints              visual_odometry_v3.py:265
@@ -57,6 +59,26 @@ def bf_match(dq: np.ndarray, dt: np.ndarray, cross_check: int = 1, ctx=None) -> 
     c.check(c.lib.dvo_bf_match_hamming(c.h, ptr(dq), len(dq), ptr(dt), len(dt), int(cross_check), ptr(out), len(out),
                                        ctypes.byref(m)))
     return out[:m.value].copy()
+
+
+NORM_L1, NORM_L2SQR = 0, 1
+
+
+def bf_knn_float(dq: np.ndarray, dt: np.ndarray, k: int = 2, norm: int = NORM_L1, ctx=None):
+    """k nearest trains of each float query: (train_idx int32[nq, k], dist
+    float32[nq, k]) in OpenCV's order (ascending distance, lower train index
+    first on ties); -1 / FLT_MAX pad queries with fewer than k trains.
+    norm NORM_L1 (BFMatcher(NORM_L1)) or NORM_L2SQR (FLANN's squared L2)."""
+    c = _ctx(ctx)
+    dq = np.ascontiguousarray(dq, np.float32)
+    dt = np.ascontiguousarray(dt, np.float32)
+    if dq.ndim != 2 or dt.ndim != 2 or (len(dt) and dt.shape[1] != dq.shape[1]):
+        raise DVOError(-1, "descriptors must be float32[n, dim] with the same dim")
+    nq, nt, dim = dq.shape[0], dt.shape[0], dq.shape[1]
+    idx = np.zeros((max(nq, 1), k), np.int32)
+    dist = np.zeros((max(nq, 1), k), np.float32)
+    c.check(c.lib.dvo_bf_knn_float(c.h, ptr(dq), nq, ptr(dt), nt, dim, int(k), int(norm), ptr(idx), ptr(dist)))
+    return idx[:nq].copy(), dist[:nq].copy()
 
 
 def _pts(p):

@@ -76,6 +76,21 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
 int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int cross_check,
                          dvo_dmatch* out, int cap, int* m_out);
 
+/* Replaces cv::BFMatcher(NORM_L1).knnMatch(query, train, k) (k = 1: .match) on
+ * float descriptors — the SIFT/SURF modes, visual_odometry_v3.py:99-106
+ * (construction) and :200-204, :214-215 (calls) — and, with DVO_NORM_L2SQR,
+ * serves cv::FlannBasedMatcher(KDTREE).knnMatch (:206-212) by exact search
+ * (FLANN reports squared L2; its randomized kd-trees are approximate, so
+ * exact results are the FLANN result whenever FLANN finds the true
+ * neighbours).  dq: nq x dim, dt: nt x dim floats, dim 64 (SURF) or 128
+ * (SIFT), k 1..4.  Per query, train_idx/dist get k entries in OpenCV's
+ * order (ascending distance, lower train index first on ties); -1 / FLT_MAX
+ * pad queries with fewer than k trains. */
+#define DVO_NORM_L1 0
+#define DVO_NORM_L2SQR 1
+int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
+                     int32_t* train_idx, float* dist);
+
 /* Replaces cv::findEssentialMat(points1, points2, K, RANSAC, prob, threshold,
  * maxIters) — visual_odometry_v3.py:297-300.  p1/p2: m x 2 doubles (pixel
  * coords, the float32 KeyPoint_convert output widened).  E receives 3 rows

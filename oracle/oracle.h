@@ -52,6 +52,12 @@ int ora_bf_match_hamming(const uint8_t* dq, int nq, const uint8_t* dt, int nt,
                          int mode, int32_t* qidx, int32_t* tidx, float* dist,
                          int* m_out);
 
+// ---- BFMatcher(NORM_L1).knnMatch / FLANN stand-in on float descriptors ------
+// norm 0: L1 (cv::normL1), 1: squared L2 (flann::L2).  tidx/dist: nq x k,
+// -1 / FLT_MAX where fewer than k trains exist.
+int ora_bf_knn_float(const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
+                     int32_t* tidx, float* dist);
+
 // ---- findEssentialMat(RANSAC) / recoverPose / triangulatePoints -------------
 // E_out holds up to 10 stacked 3x3 models (only when m == 5); *rows = 3*k.
 // Returns 0 on success, <0 on failure (E empty).

@@ -52,6 +52,7 @@ def lib():
             "ora_retain_best_depth": [_f32p, _c, _c, _c, _i32p],
             "ora_orb_detect_and_compute": [_u8p, _c, _c, _c, _c, _kpp, _u8p, _c, _ip],
             "ora_bf_match_hamming": [_u8p, _c, _u8p, _c, _c, _i32p, _i32p, _f32p, _ip],
+            "ora_bf_knn_float": [_f32p, _c, _f32p, _c, _c, _c, _c, _i32p, _f32p],
             "ora_find_essential": [_f64p, _f64p, _c, _f64p, _d, _d, _c, _f64p, _ip, _u8p, _ip],
             "ora_recover_pose": [_f64p, _f64p, _f64p, _c, _f64p, _d, ctypes.c_void_p, _f64p, _f64p, _u8p, _ip],
             "ora_triangulate": [_f64p, _f64p, _f64p, _f64p, _c, _f64p],
@@ -142,6 +143,20 @@ def bf_match(dq, dt, mode=1):
                                ctypes.byref(m))
     k = m.value
     return q[:k].copy(), t[:k].copy(), d[:k].copy()
+
+
+def bf_knn_float(dq, dt, k=2, norm=0):
+    """(train_idx int32[nq, k], dist float32[nq, k]); norm 0 = L1, 1 = squared L2."""
+    dq = np.ascontiguousarray(dq, np.float32)
+    dt = np.ascontiguousarray(dt, np.float32)
+    nq, nt = len(dq), len(dt)
+    dim = dq.shape[1] if dq.ndim == 2 else dt.shape[1]
+    idx = np.zeros((max(nq, 1), k), np.int32)
+    dist = np.zeros((max(nq, 1), k), np.float32)
+    rc = lib().ora_bf_knn_float(dq.reshape(-1) if nq else np.zeros(dim, np.float32), nq,
+                                dt.reshape(-1) if nt else np.zeros(dim, np.float32), nt, dim, k, norm, idx, dist)
+    assert rc == 0, rc
+    return idx[:nq].copy(), dist[:nq].copy()
 
 
 def find_essential(p1, p2, K, prob=0.999, threshold=1.0, max_iters=1000):
