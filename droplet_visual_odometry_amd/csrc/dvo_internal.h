@@ -214,10 +214,11 @@ hipError_t launch_pose_tail(const double* Rt /*[pairs][12]*/, const int32_t* inf
                             const double* K, const double* cprev, const double* ccur, int k, double marker_length,
                             double* carry, double* T_rel, double* T_abs, hipStream_t s);
 hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
-// Float-descriptor kNN (NORM_L1 / squared L2), dim 64 or 128, k 1..4.  d_part /
-// d_pidx: knn_chunks(nt) * nq * k partial slots (unused when one chunk).
-int knn_chunks(int nt);
-hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm,
+// Float-descriptor kNN (NORM_L1 / squared L2), dim 64 or 128, k 1..4, over
+// `ranges` = knn_ranges(nq, nt, CU count) train ranges; d_part / d_pidx hold
+// ranges * nq * k partial slots (unused when ranges == 1).
+int knn_ranges(int nq, int nt, int cus);
+hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm, int ranges,
                             float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);

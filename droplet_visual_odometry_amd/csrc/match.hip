@@ -14,7 +14,9 @@
 // directions run in the same launch (grid.y).
 // crosscheck_sort_kernel: mutual-NN filter, then a bitonic sort of the unique
 // keys (distance << 16 | queryIdx) in LDS, then the point gather.
+#include <algorithm>
 #include <cfloat>
+#include <climits>
 
 #include "dvo_internal.h"
 
@@ -504,31 +506,39 @@ hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int
 
 // ---- float descriptors: BFMatcher(NORM_L1).knnMatch / FLANN stand-in ---------
 // The SIFT/SURF branches (visual_odometry_v3.py:99-106, :200-215).  One thread
-// per query holds its descriptor in registers; a workgroup scans a chunk of
-// kKnnTC trains whose rows are wave-uniform, so they arrive through scalar
-// loads (SGPR operands of the VALU ops, no LDS or per-lane traffic).  Grid:
-// x = query blocks, y = train chunks; each (query, chunk) keeps its K best in
-// OpenCV's batchDistance order (enter iff d < dist[K-1], land after entries
-// with dist <= d), and a merge kernel folds the chunks in train order, which
-// reproduces the sequential scan exactly (oracle ora_bf_knn_float).
+// per query holds its descriptor in registers; a workgroup scans a contiguous
+// train range, staging kKnnTC rows at a time in LDS, which every wave reads
+// as wave-uniform (broadcast) ds_read_b128 through a software pipeline
+// (scalar loads of the rows serialised on their latency: 13x off).  Grid:
+// x = query blocks, y = train ranges, sized so the grid is about one round of
+// resident workgroups (3 per CU at <= 168 VGPRs): a fixed 64-row split left a
+// third round nearly empty.  Each (query, range) keeps its K best in OpenCV's
+// batchDistance order (enter iff d < dist[K-1], land after entries with
+// dist <= d), i.e. the K smallest (distance, train index) pairs in
+// lexicographic order; a merge kernel folds the ranges with a wave per query
+// (that order is total, so any merge tree gives the sequential scan's result;
+// oracle ora_bf_knn_float).
 namespace {
 
 constexpr int kKnnQ = 256;  // queries per workgroup (one per thread)
-constexpr int kKnnTC = 64;  // trains per workgroup
+constexpr int kKnnTC = 64;  // train rows per LDS stage
+constexpr int kKnnWgPerCu = 3;
+#ifndef DVO_KNN_G
+#define DVO_KNN_G 2
+#endif
+constexpr int kKnnG = DVO_KNN_G;  // float4 train pieces in flight per wave (software pipeline depth)
 
-template <int D, int NORM>
-__device__ __forceinline__ float desc_distance(const float (&q)[D], const float* __restrict__ t) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < D; i += 4) {
-        const float d0 = q[i] - t[i], d1 = q[i + 1] - t[i + 1], d2 = q[i + 2] - t[i + 2], d3 = q[i + 3] - t[i + 3];
-        if constexpr (NORM == 0) {
-            s += ((fabsf(d0) + fabsf(d1)) + fabsf(d2)) + fabsf(d3);  // cv::normL1 (base.hpp)
-        } else {
-            s += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;  // flann::L2 (no contraction: -ffp-contract=off)
-        }
+// One group of 4 descriptor elements into the running distance: cv::normL1
+// (base.hpp: s += |v0| + |v1| + |v2| + |v3|) or flann::L2 (squared, same
+// grouping); no contraction under -ffp-contract=off.
+template <int NORM>
+__device__ __forceinline__ void dist_group(float& s, float a0, float a1, float a2, float a3, const float4 tv) {
+    const float d0 = a0 - tv.x, d1 = a1 - tv.y, d2 = a2 - tv.z, d3 = a3 - tv.w;
+    if constexpr (NORM == 0) {
+        s += ((fabsf(d0) + fabsf(d1)) + fabsf(d2)) + fabsf(d3);
+    } else {
+        s += ((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3;
     }
-    return s;
 }
 
 template <int K>
@@ -552,14 +562,17 @@ __device__ __forceinline__ void knn_insert(float (&bd)[K], int (&bi)[K], float d
 
 template <int D, int NORM, int K>
 __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restrict__ q, int nq,
-                                                          const float* __restrict__ t, int nt,
+                                                          const float* __restrict__ t, int nt, int range,
                                                           float* __restrict__ odist, int32_t* __restrict__ oidx) {
+    constexpr int R = D / 4;
+    static_assert(R % kKnnG == 0, "pipeline depth must divide the row");
+    __shared__ float4 st[kKnnTC * R];
     const int qi = blockIdx.x * kKnnQ + threadIdx.x;
     const int qs = qi < nq ? qi : nq - 1;  // clamped: spare lanes compute, never store
     float qv[D];
     const float4* q4 = reinterpret_cast<const float4*>(q + (size_t)qs * D);
 #pragma unroll
-    for (int i = 0; i < D / 4; ++i) {
+    for (int i = 0; i < R; ++i) {
         const float4 v = q4[i];
         qv[4 * i] = v.x;
         qv[4 * i + 1] = v.y;
@@ -573,8 +586,41 @@ __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restric
         bd[s] = FLT_MAX;
         bi[s] = -1;
     }
-    const int j0 = blockIdx.y * kKnnTC, j1 = min(nt, j0 + kKnnTC);
-    for (int j = j0; j < j1; ++j) knn_insert<K>(bd, bi, desc_distance<D, NORM>(qv, t + (size_t)j * D), j);
+    const int r0 = blockIdx.y * range, r1 = min(nt, r0 + range);
+    for (int j0 = r0; j0 < r1; j0 += kKnnTC) {
+        const int nj = min(r1 - j0, kKnnTC);
+        const float4* src = reinterpret_cast<const float4*>(t + (size_t)j0 * D);
+        if (j0 != r0) __syncthreads();  // previous stage fully read
+        for (int i = threadIdx.x; i < nj * R; i += kKnnQ) st[i] = src[i];
+        __syncthreads();
+        // software pipeline over the stage's float4 stream: the next kKnnG
+        // pieces (of this row or the next) are read while the current ones
+        // are consumed
+        float4 cur[kKnnG];
+#pragma unroll
+        for (int e = 0; e < kKnnG; ++e) cur[e] = st[e];
+        for (int j = 0; j < nj; ++j) {
+            const float4* row = st + j * R;
+            const float4* nrow = st + min(j + 1, nj - 1) * R;
+            float s = 0.f;
+#pragma unroll
+            for (int g = 0; g < R; g += kKnnG) {
+                float4 nxt[kKnnG];
+                const float4* pf = g + kKnnG < R ? row + g + kKnnG : nrow;
+#pragma unroll
+                for (int e = 0; e < kKnnG; ++e) nxt[e] = pf[e];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int e = 0; e < kKnnG; ++e) {
+                    const int i = 4 * (g + e);
+                    dist_group<NORM>(s, qv[i], qv[i + 1], qv[i + 2], qv[i + 3], cur[e]);
+                }
+#pragma unroll
+                for (int e = 0; e < kKnnG; ++e) cur[e] = nxt[e];
+            }
+            knn_insert<K>(bd, bi, s, j0 + j);
+        }
+    }
     if (qi < nq) {
         const size_t o = ((size_t)blockIdx.y * nq + qi) * K;
 #pragma unroll
@@ -585,72 +631,148 @@ __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restric
     }
 }
 
+// (d, i) lexicographic; empty slots are (FLT_MAX, INT_MAX) and sort last
+__device__ __forceinline__ bool knn_less(float da, int ia, float db, int ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+// K smallest of two sorted K-lists, in place into (ad, ai)
+template <int K>
+__device__ __forceinline__ void knn_merge2(float (&ad)[K], int (&ai)[K], const float (&bd)[K], const int (&bi)[K]) {
+    float md[K];
+    int mi[K];
+    int pa = 0, pb = 0;
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        float da = FLT_MAX, db = FLT_MAX;
+        int ia = INT_MAX, ib = INT_MAX;
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            if (u == pa) { da = ad[u]; ia = ai[u]; }
+            if (u == pb) { db = bd[u]; ib = bi[u]; }
+        }
+        const bool ta = knn_less(da, ia, db, ib);
+        md[s] = ta ? da : db;
+        mi[s] = ta ? ia : ib;
+        pa += ta;
+        pb += !ta;
+    }
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+        ad[s] = md[s];
+        ai[s] = mi[s];
+    }
+}
+
+// one wave per query: lane l folds ranges l, l+64, ... by sequential
+// insertion, then a butterfly of sorted-list merges
 template <int K>
 __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
-                                                        int nq, int chunks, float* __restrict__ odist,
+                                                        int nq, int ranges, float* __restrict__ odist,
                                                         int32_t* __restrict__ oidx) {
-    const int qi = blockIdx.x * 256 + threadIdx.x;
-    if (qi >= nq) return;
+    const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (qi >= nq) return;  // wave-uniform
     float bd[K];
     int bi[K];
 #pragma unroll
     for (int s = 0; s < K; ++s) {
         bd[s] = FLT_MAX;
-        bi[s] = -1;
+        bi[s] = INT_MAX;
     }
-    for (int c = 0; c < chunks; ++c) {
+    for (int c = lane; c < ranges; c += 64) {
         const size_t o = ((size_t)c * nq + qi) * K;
+        float cd[K];
+        int ci[K];
 #pragma unroll
-        for (int s = 0; s < K; ++s)
-            if (pidx[o + s] >= 0) knn_insert<K>(bd, bi, pdist[o + s], pidx[o + s]);
+        for (int s = 0; s < K; ++s) {
+            const int i = pidx[o + s];
+            cd[s] = i >= 0 ? pdist[o + s] : FLT_MAX;
+            ci[s] = i >= 0 ? i : INT_MAX;
+        }
+        knn_merge2<K>(bd, bi, cd, ci);
     }
 #pragma unroll
-    for (int s = 0; s < K; ++s) {
-        odist[(size_t)qi * K + s] = bd[s];
-        oidx[(size_t)qi * K + s] = bi[s];
+    for (int m = 1; m < 64; m <<= 1) {
+        float od[K];
+        int oi[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            od[s] = __shfl_xor(bd[s], m, 64);
+            oi[s] = __shfl_xor(bi[s], m, 64);
+        }
+        knn_merge2<K>(bd, bi, od, oi);
+    }
+    if (lane < K) {
+        float d = bd[0];
+        int i = bi[0];
+#pragma unroll
+        for (int s = 1; s < K; ++s)
+            if (lane == s) {
+                d = bd[s];
+                i = bi[s];
+            }
+        odist[(size_t)qi * K + lane] = i == INT_MAX ? FLT_MAX : d;
+        oidx[(size_t)qi * K + lane] = i == INT_MAX ? -1 : i;
     }
 }
 
 template <int D, int NORM, int K>
-hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, float* d_part, int32_t* d_pidx,
-                        float* d_dist, int32_t* d_idx, hipStream_t s) {
-    const int chunks = (nt + kKnnTC - 1) / kKnnTC;
-    const dim3 grid((nq + kKnnQ - 1) / kKnnQ, chunks);
-    if (chunks == 1) {
-        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, d_dist, d_idx);
+hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, int ranges, float* d_part,
+                        int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
+    const int range = (nt + ranges - 1) / ranges;
+    const dim3 grid((nq + kKnnQ - 1) / kKnnQ, ranges);
+    if (ranges == 1) {
+        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, range, d_dist,
+                           d_idx);
     } else {
-        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, d_part, d_pidx);
-        hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 255) / 256), dim3(256), 0, s, d_part, d_pidx, nq, chunks,
+        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, range, d_part,
+                           d_pidx);
+        hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 3) / 4), dim3(256), 0, s, d_part, d_pidx, nq, ranges,
                            d_dist, d_idx);
     }
     return hipGetLastError();
 }
 
 template <int D, int NORM>
-hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int nt, float* d_part, int32_t* d_pidx,
-                        float* d_dist, int32_t* d_idx, hipStream_t s) {
+hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int nt, int ranges, float* d_part,
+                        int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
     switch (k) {
-        case 1: return launch_knn_t<D, NORM, 1>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
-        case 2: return launch_knn_t<D, NORM, 2>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
-        case 3: return launch_knn_t<D, NORM, 3>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
-        case 4: return launch_knn_t<D, NORM, 4>(d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        case 1: return launch_knn_t<D, NORM, 1>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        case 2: return launch_knn_t<D, NORM, 2>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        case 3: return launch_knn_t<D, NORM, 3>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        case 4: return launch_knn_t<D, NORM, 4>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
 
-int knn_chunks(int nt) { return (nt + kKnnTC - 1) / kKnnTC; }
+int knn_ranges(int nq, int nt, int cus) {
+    // about one round of resident workgroups, at least 16 trains per range
+    const int qblocks = (nq + kKnnQ - 1) / kKnnQ;
+#ifndef DVO_KNN_ROUNDS
+#define DVO_KNN_ROUNDS 2
+#endif
+#ifdef DVO_KNN_FIXED
+    int ranges = (nt + kKnnTC - 1) / kKnnTC;
+#else
+    int ranges = (cus * kKnnWgPerCu * DVO_KNN_ROUNDS) / qblocks;
+#endif
+    ranges = std::min(ranges, (nt + 15) / 16);
+    ranges = std::max(ranges, 1);
+    const int range = (nt + ranges - 1) / ranges;
+    return (nt + range - 1) / range;  // no empty trailing range
+}
 
-hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm,
+hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm, int ranges,
                             float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
     if (nq <= 0 || nt <= 0) return hipSuccess;
     if (dim == 128)
-        return norm == 0 ? launch_knn_k<128, 0>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s)
-                         : launch_knn_k<128, 1>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        return norm == 0 ? launch_knn_k<128, 0>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<128, 1>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
     if (dim == 64)
-        return norm == 0 ? launch_knn_k<64, 0>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s)
-                         : launch_knn_k<64, 1>(k, d_q, nq, d_t, nt, d_part, d_pidx, d_dist, d_idx, s);
+        return norm == 0 ? launch_knn_k<64, 0>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<64, 1>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
     return hipErrorInvalidValue;
 }
 

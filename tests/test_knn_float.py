@@ -112,7 +112,8 @@ def test_gpu_knn_bit_exact_real_valued(gpu_ctx, oracle_mod, norm):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nq,nt", [(1, 1), (1, 2), (3, 1), (257, 63), (256, 64), (255, 65), (5000, 4000)])
+@pytest.mark.parametrize("nq,nt", [(1, 1), (1, 2), (3, 1), (257, 63), (256, 64), (255, 65), (5000, 4000),
+                                   (20000, 1500)])
 def test_gpu_knn_sizes(gpu_ctx, oracle_mod, nq, nt):
     from droplet_visual_odometry_amd import ops
     rng = np.random.default_rng(nq * 7 + nt)
