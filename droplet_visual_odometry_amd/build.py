@@ -30,6 +30,11 @@ CXXFLAGS = [
     "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
 ]
 
+# Per-file code generation: the matcher's MFMA accumulators in VGPRs (no
+# v_accvgpr_read of 32 accumulators per 32 trains before the epilogue; match
+# stage 1.52 -> 1.43 ms per 1024 pairs, tools/ab_stages.sh).
+FILE_FLAGS = {"match.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
 
 def _torch_lib_dir():
     try:
@@ -72,7 +77,8 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     def compile_one(pair):
         src, obj = pair
         lang = ["-x", "hip"]
-        cmd = [hipcc, *lang, *CXXFLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
+        extra = [t for d in defines for t in (d.split() if d.startswith("-") else [f"-D{d}"])]  # raw flags pass through
+        cmd = [hipcc, *lang, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
