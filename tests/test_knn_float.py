@@ -194,3 +194,26 @@ def test_dropin_ratio_modes(gpu_ctx, oracle_mod, mode):
     assert len(matches) == 300 and len(keep) >= 150
     assert [kp.pt[0] for kp in top_prev] == [float(q) for q in keep]
     assert [kp.pt[0] for kp in top_cur] == [float(idx[q, 0]) for q in keep]
+
+
+@pytest.mark.gpu
+def test_dropin_sift_mode_fails_in_ratio_loop_like_the_reference(gpu_ctx):
+    """'sift' mode calls bf.match (v3:200-201) and then unpacks `for m, n in
+    matches` (v3:226): single DMatch objects do not unpack into two, so the
+    reference raises there (cv2: TypeError); the drop-in raises too."""
+    import os
+    import sys
+    import types
+    from droplet_visual_odometry_amd import cv
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "droplet_visual_odometry_amd", "dropin"))
+    try:
+        import visual_odometry_v3 as v3
+    finally:
+        sys.path.pop(0)
+    rng = np.random.default_rng(1)
+    d = sift_like(rng, 20)
+    kps = [cv.KeyPoint(float(i), 0.0) for i in range(20)]
+    me = types.SimpleNamespace(mode="sift", bf=cv.BFMatcher(normType=cv.NORM_L1, crossCheck=False))
+    with pytest.raises((TypeError, ValueError)):
+        v3.VisualOdometry.get_matches_between_two_frames(me, kps, d, kps, d)
