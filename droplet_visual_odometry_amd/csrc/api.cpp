@@ -709,15 +709,16 @@ int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
     const int ranges = knn_ranges(nq, nt, cus);
     const size_t out_n = (size_t)nq * k, part_n = ranges > 1 ? (size_t)ranges * nq * k : 1;
-    void *bq, *bt, *bd, *bi, *bpd, *bpi;
+    void *bq, *bt, *bd, *bi, *bpd, *bpi, *bb;
     int rc;
     if ((rc = scratch(ctx, 27, (size_t)nq * dim * 4, &bq)) || (rc = scratch(ctx, 28, (size_t)nt * dim * 4, &bt)) ||
         (rc = scratch(ctx, 29, out_n * 4, &bd)) || (rc = scratch(ctx, 30, out_n * 4, &bi)) ||
-        (rc = scratch(ctx, 31, part_n * 4, &bpd)) || (rc = scratch(ctx, 32, part_n * 4, &bpi)))
+        (rc = scratch(ctx, 31, part_n * 4, &bpd)) || (rc = scratch(ctx, 32, part_n * 4, &bpi)) ||
+        (rc = scratch(ctx, 33, knn_bytes_size(nq, nt, dim), &bb)))
         return rc;
     HIP_TRY(hipMemcpyAsync(bq, dq, (size_t)nq * dim * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(bt, dt, (size_t)nt * dim * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(launch_knn_float((const float*)bq, nq, (const float*)bt, nt, dim, k, norm, ranges, (float*)bpd, (int32_t*)bpi,
+    HIP_TRY(launch_knn_float((const float*)bq, nq, (const float*)bt, nt, dim, k, norm, ranges, bb, (float*)bpd, (int32_t*)bpi,
                              (float*)bd, (int32_t*)bi, ctx->stream));
     HIP_TRY(hipMemcpyAsync(dist, bd, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(train_idx, bi, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));

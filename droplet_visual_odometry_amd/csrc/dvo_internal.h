@@ -218,8 +218,11 @@ hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x 
 // `ranges` = knn_ranges(nq, nt, CU count) train ranges; d_part / d_pidx hold
 // ranges * nq * k partial slots (unused when ranges == 1).
 int knn_ranges(int nq, int nt, int cus);
+// d_bytes: knn_bytes_size(nq, nt, dim) bytes of workspace for the byte-valued fast path.
+size_t knn_bytes_size(int nq, int nt, int dim);
 hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm, int ranges,
-                            float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s);
+                            void* d_bytes, float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx,
+                            hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,

@@ -520,6 +520,11 @@ hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int
 // oracle ora_bf_knn_float).
 namespace {
 
+struct KnnBytes {  // byte-packed rows, squared norms, rejection flag (knn_pack_u8_kernel)
+    uint32_t *q, *t, *qn, *tn;
+    int* rejected;
+};
+
 constexpr int kKnnQ = 256;  // queries per workgroup (one per thread)
 constexpr int kKnnTC = 64;  // train rows per LDS stage
 constexpr int kKnnWgPerCu = 3;
@@ -563,7 +568,9 @@ __device__ __forceinline__ void knn_insert(float (&bd)[K], int (&bi)[K], float d
 template <int D, int NORM, int K>
 __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restrict__ q, int nq,
                                                           const float* __restrict__ t, int nt, int range,
+                                                          const int* __restrict__ u8_rejected,
                                                           float* __restrict__ odist, int32_t* __restrict__ oidx) {
+    if (*u8_rejected == 0) return;  // knn_u8_kernel served this call (uniform)
     constexpr int R = D / 4;
     static_assert(R % kKnnG == 0, "pipeline depth must divide the row");
     __shared__ float4 st[kKnnTC * R];
@@ -629,6 +636,131 @@ __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restric
             oidx[o + s] = bi[s];
         }
     }
+}
+
+// ---- byte-valued descriptors (SIFT: integers 0..255 stored as float) --------
+// Every partial sum of such a distance is an integer below 2^24, so any
+// summation order gives the float the restated order gives (oracle
+// ora_bf_knn_float).  knn_pack_u8_kernel packs each row into bytes and its
+// squared norm, and flags any value that is not an integer in [0, 255]; when
+// nothing is flagged, knn_u8_kernel computes the distances in integer
+// arithmetic — L1 with v_sad_u8 (4 elements per instruction), squared L2 as
+// |q|^2 + |t|^2 - 2 q.t with v_dot4_u32_u8 — kKnnU8Q queries per thread so
+// each broadcast train read feeds several rows; otherwise knn_float_kernel runs.  Both
+// fill the same (range, query) partial slots.
+// one thread per 4 values (coalesced float4 reads); a row's dim/4 threads are
+// consecutive lanes, which reduce its squared norm with xor shuffles
+__global__ __launch_bounds__(256) void knn_pack_u8_kernel(const float* __restrict__ x, int n, int dim,
+                                                          uint32_t* __restrict__ out, uint32_t* __restrict__ norm,
+                                                          int* __restrict__ rejected) {
+    const int wpr = dim / 4;  // 16 or 32: divides 64
+    const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool in = id < (int64_t)n * wpr;
+    const float4 v = in ? reinterpret_cast<const float4*>(x)[id] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    uint32_t word = 0, ss = 0;
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        ok &= e[c] >= 0.f && e[c] <= 255.f && e[c] == __builtin_rintf(e[c]);  // NaN fails
+        const uint32_t b = e[c] >= 0.f && e[c] <= 255.f ? (uint32_t)e[c] : 0u;
+        word |= b << (8 * c);
+        ss += b * b;
+    }
+    for (int o = 1; o < wpr; o <<= 1) ss += __shfl_xor(ss, o);
+    if (in) {
+        out[id] = word;
+        if ((id & (wpr - 1)) == 0) norm[id / wpr] = ss;
+    }
+    if (__ballot(!ok) != 0 && (threadIdx.x & 63) == 0) atomicOr(rejected, 1);
+}
+
+#ifndef DVO_KNN_U8Q
+#define DVO_KNN_U8Q 2
+#endif
+constexpr int kKnnU8Q = DVO_KNN_U8Q;  // queries per thread in knn_u8_kernel
+
+template <int D, int NORM, int K>
+__global__ __launch_bounds__(256) void knn_u8_kernel(const uint32_t* __restrict__ q, const uint32_t* __restrict__ qn,
+                                                     int nq, const uint32_t* __restrict__ t,
+                                                     const uint32_t* __restrict__ tn, int nt, int range,
+                                                     const int* __restrict__ rejected, float* __restrict__ odist,
+                                                     int32_t* __restrict__ oidx) {
+    if (*rejected != 0) return;  // some value is not a byte: knn_float_kernel serves the call (uniform)
+    constexpr int W = D / 16;    // uint4 per row
+    __shared__ uint4 st[kKnnTC * W];
+    __shared__ uint32_t stn[kKnnTC];
+    int qi[kKnnU8Q];
+    uint4 qv[kKnnU8Q][W];
+    uint32_t qnv[kKnnU8Q];
+    float bd[kKnnU8Q][K];
+    int bi[kKnnU8Q][K];
+#pragma unroll
+    for (int u = 0; u < kKnnU8Q; ++u) {
+        qi[u] = blockIdx.x * (256 * kKnnU8Q) + 256 * u + threadIdx.x;
+        const int qs = qi[u] < nq ? qi[u] : nq - 1;
+        const uint4* q4 = reinterpret_cast<const uint4*>(q + (size_t)qs * (D / 4));
+#pragma unroll
+        for (int g = 0; g < W; ++g) qv[u][g] = q4[g];
+        qnv[u] = qn[qs];
+#pragma unroll
+        for (int s2 = 0; s2 < K; ++s2) {
+            bd[u][s2] = FLT_MAX;
+            bi[u][s2] = -1;
+        }
+    }
+    const int r0 = blockIdx.y * range, r1 = min(nt, r0 + range);
+    for (int j0 = r0; j0 < r1; j0 += kKnnTC) {
+        const int nj = min(r1 - j0, kKnnTC);
+        const uint4* src = reinterpret_cast<const uint4*>(t + (size_t)j0 * (D / 4));
+        if (j0 != r0) __syncthreads();
+        for (int i = threadIdx.x; i < nj * W; i += 256) st[i] = src[i];
+        if (threadIdx.x < nj) stn[threadIdx.x] = tn[j0 + threadIdx.x];
+        __syncthreads();
+        uint4 cur[W];
+#pragma unroll
+        for (int g = 0; g < W; ++g) cur[g] = st[g];
+        for (int j = 0; j < nj; ++j) {
+            uint4 nxt[W];
+            const uint4* nrow = st + min(j + 1, nj - 1) * W;
+#pragma unroll
+            for (int g = 0; g < W; ++g) nxt[g] = nrow[g];
+            const uint32_t tnj = stn[j];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < kKnnU8Q; ++u) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int g = 0; g < W; ++g) {
+                    if constexpr (NORM == 0) {
+                        acc = __builtin_amdgcn_sad_u8(qv[u][g].x, cur[g].x, acc);
+                        acc = __builtin_amdgcn_sad_u8(qv[u][g].y, cur[g].y, acc);
+                        acc = __builtin_amdgcn_sad_u8(qv[u][g].z, cur[g].z, acc);
+                        acc = __builtin_amdgcn_sad_u8(qv[u][g].w, cur[g].w, acc);
+                    } else {
+                        acc = __builtin_amdgcn_udot4(qv[u][g].x, cur[g].x, acc, false);
+                        acc = __builtin_amdgcn_udot4(qv[u][g].y, cur[g].y, acc, false);
+                        acc = __builtin_amdgcn_udot4(qv[u][g].z, cur[g].z, acc, false);
+                        acc = __builtin_amdgcn_udot4(qv[u][g].w, cur[g].w, acc, false);
+                    }
+                }
+                const uint32_t d = NORM == 0 ? acc : qnv[u] + tnj - 2u * acc;  // exact: < 2^24
+                knn_insert<K>(bd[u], bi[u], (float)d, j0 + j);
+            }
+#pragma unroll
+            for (int g = 0; g < W; ++g) cur[g] = nxt[g];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kKnnU8Q; ++u)
+        if (qi[u] < nq) {
+            const size_t o = ((size_t)blockIdx.y * nq + qi[u]) * K;
+#pragma unroll
+            for (int s2 = 0; s2 < K; ++s2) {
+                odist[o + s2] = bd[u][s2];
+                oidx[o + s2] = bi[u][s2];
+            }
+        }
 }
 
 // (d, i) lexicographic; empty slots are (FLT_MAX, INT_MAX) and sort last
@@ -717,30 +849,35 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict_
 }
 
 template <int D, int NORM, int K>
-hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, int ranges, float* d_part,
-                        int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
+hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, int ranges, const KnnBytes& u8,
+                        float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
     const int range = (nt + ranges - 1) / ranges;
-    const dim3 grid((nq + kKnnQ - 1) / kKnnQ, ranges);
-    if (ranges == 1) {
-        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, range, d_dist,
-                           d_idx);
-    } else {
-        hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), grid, dim3(kKnnQ), 0, s, d_q, nq, d_t, nt, range, d_part,
-                           d_pidx);
+    float* od = ranges == 1 ? d_dist : d_part;
+    int32_t* oi = ranges == 1 ? d_idx : d_pidx;
+    hipError_t e = hipMemsetAsync(u8.rejected, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(knn_pack_u8_kernel, dim3((int)(((int64_t)nq * (D / 4) + 255) / 256)), dim3(256), 0, s, d_q, nq,
+                       D, u8.q, u8.qn, u8.rejected);
+    hipLaunchKernelGGL(knn_pack_u8_kernel, dim3((int)(((int64_t)nt * (D / 4) + 255) / 256)), dim3(256), 0, s, d_t, nt,
+                       D, u8.t, u8.tn, u8.rejected);
+    hipLaunchKernelGGL((knn_u8_kernel<D, NORM, K>), dim3((nq + 256 * kKnnU8Q - 1) / (256 * kKnnU8Q), ranges), dim3(256), 0, s, u8.q, u8.qn, nq,
+                       u8.t, u8.tn, nt, range, u8.rejected, od, oi);
+    hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), dim3((nq + kKnnQ - 1) / kKnnQ, ranges), dim3(kKnnQ), 0, s, d_q,
+                       nq, d_t, nt, range, u8.rejected, od, oi);
+    if (ranges > 1)
         hipLaunchKernelGGL((knn_merge_kernel<K>), dim3((nq + 3) / 4), dim3(256), 0, s, d_part, d_pidx, nq, ranges,
                            d_dist, d_idx);
-    }
     return hipGetLastError();
 }
 
 template <int D, int NORM>
-hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int nt, int ranges, float* d_part,
-                        int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
+hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int nt, int ranges, const KnnBytes& u8,
+                        float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
     switch (k) {
-        case 1: return launch_knn_t<D, NORM, 1>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
-        case 2: return launch_knn_t<D, NORM, 2>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
-        case 3: return launch_knn_t<D, NORM, 3>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
-        case 4: return launch_knn_t<D, NORM, 4>(d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        case 1: return launch_knn_t<D, NORM, 1>(d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
+        case 2: return launch_knn_t<D, NORM, 2>(d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
+        case 3: return launch_knn_t<D, NORM, 3>(d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
+        case 4: return launch_knn_t<D, NORM, 4>(d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -764,15 +901,25 @@ int knn_ranges(int nq, int nt, int cus) {
     return (nt + range - 1) / range;  // no empty trailing range
 }
 
+size_t knn_bytes_size(int nq, int nt, int dim) { return (size_t)(nq + nt) * dim + 4 * (size_t)(nq + nt) + 16; }
+
 hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm, int ranges,
-                            float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx, hipStream_t s) {
+                            void* d_bytes, float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx,
+                            hipStream_t s) {
     if (nq <= 0 || nt <= 0) return hipSuccess;
+    uint8_t* b = static_cast<uint8_t*>(d_bytes);  // packed rows (dim bytes each; dim % 64 == 0), norms, flag
+    KnnBytes u8;
+    u8.q = reinterpret_cast<uint32_t*>(b);
+    u8.t = reinterpret_cast<uint32_t*>(b + (size_t)nq * dim);
+    u8.qn = reinterpret_cast<uint32_t*>(b + (size_t)(nq + nt) * dim);
+    u8.tn = u8.qn + nq;
+    u8.rejected = reinterpret_cast<int*>(u8.tn + nt);
     if (dim == 128)
-        return norm == 0 ? launch_knn_k<128, 0>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s)
-                         : launch_knn_k<128, 1>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        return norm == 0 ? launch_knn_k<128, 0>(k, d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<128, 1>(k, d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
     if (dim == 64)
-        return norm == 0 ? launch_knn_k<64, 0>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s)
-                         : launch_knn_k<64, 1>(k, d_q, nq, d_t, nt, ranges, d_part, d_pidx, d_dist, d_idx, s);
+        return norm == 0 ? launch_knn_k<64, 0>(k, d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s)
+                         : launch_knn_k<64, 1>(k, d_q, nq, d_t, nt, ranges, u8, d_part, d_pidx, d_dist, d_idx, s);
     return hipErrorInvalidValue;
 }
 

@@ -217,3 +217,23 @@ def test_dropin_sift_mode_fails_in_ratio_loop_like_the_reference(gpu_ctx):
     me = types.SimpleNamespace(mode="sift", bf=cv.BFMatcher(normType=cv.NORM_L1, crossCheck=False))
     with pytest.raises((TypeError, ValueError)):
         v3.VisualOdometry.get_matches_between_two_frames(me, kps, d, kps, d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("poison", [255.5, 300.0, -1.0, 0.25])
+@pytest.mark.parametrize("norm", [0, 1])
+def test_gpu_knn_non_byte_values_take_the_float_path(gpu_ctx, oracle_mod, poison, norm):
+    """One value outside the byte fast path (non-integer, > 255 or negative,
+    in queries or trains) sends the whole call to the float kernel: results
+    stay bit-exact to the oracle either way."""
+    from droplet_visual_odometry_amd import ops
+    rng = np.random.default_rng(int(abs(poison) * 4) + norm)
+    dq, dt = sift_like(rng, 700), sift_like(rng, 900)
+    for a, who in [(dq, "q"), (dt, "t")]:
+        b = a.copy()
+        b[17, 33] = poison
+        q, t = (b, dt) if who == "q" else (dq, b)
+        i_g, d_g = ops.bf_knn_float(q, t, 2, norm, ctx=gpu_ctx)
+        i_o, d_o = oracle_mod.bf_knn_float(q, t, 2, norm)
+        np.testing.assert_array_equal(i_g, i_o)
+        np.testing.assert_array_equal(d_g.view(np.uint32), d_o.view(np.uint32))

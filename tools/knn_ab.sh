@@ -12,7 +12,7 @@ for v in base "$@"; do
 import csv, sys
 for r in csv.DictReader(open(sys.argv[2])):
     if "knn" in r["Name"]:
-        print(sys.argv[1], r["Name"].split("(")[0][-40:], r["Calls"], "avg_us=%.1f min_us=%.1f max_us=%.1f" % (
+        print(sys.argv[1], r["Name"].replace("(anonymous namespace)::", "").split("(")[0][-48:], r["Calls"], "avg_us=%.1f min_us=%.1f max_us=%.1f" % (
             float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3, float(r["MaxNs"]) / 1e3))
 PY
 done
