@@ -650,11 +650,18 @@ __global__ __launch_bounds__(kKnnQ) void knn_float_kernel(const float* __restric
 // fill the same (range, query) partial slots.
 // one thread per 4 values (coalesced float4 reads); a row's dim/4 threads are
 // consecutive lanes, which reduce its squared norm with xor shuffles
-__global__ __launch_bounds__(256) void knn_pack_u8_kernel(const float* __restrict__ x, int n, int dim,
-                                                          uint32_t* __restrict__ out, uint32_t* __restrict__ norm,
-                                                          int* __restrict__ rejected) {
+// One launch packs both sides: blocks [0, qblocks) take the queries, the rest the trains.
+__global__ __launch_bounds__(256) void knn_pack_u8_kernel(const float* __restrict__ xq, int nq,
+                                                          const float* __restrict__ xt, int nt, int dim, int qblocks,
+                                                          KnnBytes u8) {
+    const bool side_q = (int)blockIdx.x < qblocks;
+    const float* __restrict__ x = side_q ? xq : xt;
+    const int n = side_q ? nq : nt;
+    uint32_t* __restrict__ out = side_q ? u8.q : u8.t;
+    uint32_t* __restrict__ norm = side_q ? u8.qn : u8.tn;
+    int* __restrict__ rejected = u8.rejected;
     const int wpr = dim / 4;  // 16 or 32: divides 64
-    const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t id = (int64_t)(side_q ? blockIdx.x : blockIdx.x - qblocks) * 256 + threadIdx.x;
     const bool in = id < (int64_t)n * wpr;
     const float4 v = in ? reinterpret_cast<const float4*>(x)[id] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float e[4] = {v.x, v.y, v.z, v.w};
@@ -856,10 +863,8 @@ hipError_t launch_knn_t(const float* d_q, int nq, const float* d_t, int nt, int 
     int32_t* oi = ranges == 1 ? d_idx : d_pidx;
     hipError_t e = hipMemsetAsync(u8.rejected, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(knn_pack_u8_kernel, dim3((int)(((int64_t)nq * (D / 4) + 255) / 256)), dim3(256), 0, s, d_q, nq,
-                       D, u8.q, u8.qn, u8.rejected);
-    hipLaunchKernelGGL(knn_pack_u8_kernel, dim3((int)(((int64_t)nt * (D / 4) + 255) / 256)), dim3(256), 0, s, d_t, nt,
-                       D, u8.t, u8.tn, u8.rejected);
+    const int qblocks = (int)(((int64_t)nq * (D / 4) + 255) / 256), tblocks = (int)(((int64_t)nt * (D / 4) + 255) / 256);
+    hipLaunchKernelGGL(knn_pack_u8_kernel, dim3(qblocks + tblocks), dim3(256), 0, s, d_q, nq, d_t, nt, D, qblocks, u8);
     hipLaunchKernelGGL((knn_u8_kernel<D, NORM, K>), dim3((nq + 256 * kKnnU8Q - 1) / (256 * kKnnU8Q), ranges), dim3(256), 0, s, u8.q, u8.qn, nq,
                        u8.t, u8.tn, nt, range, u8.rejected, od, oi);
     hipLaunchKernelGGL((knn_float_kernel<D, NORM, K>), dim3((nq + kKnnQ - 1) / kKnnQ, ranges), dim3(kKnnQ), 0, s, d_q,
