@@ -237,3 +237,25 @@ def test_gpu_knn_non_byte_values_take_the_float_path(gpu_ctx, oracle_mod, poison
         i_o, d_o = oracle_mod.bf_knn_float(q, t, 2, norm)
         np.testing.assert_array_equal(i_g, i_o)
         np.testing.assert_array_equal(d_g.view(np.uint32), d_o.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm", [0, 1])
+def test_gpu_knn_byte_path_extremes(gpu_ctx, oracle_mod, norm):
+    """Byte path at its range limits: all-0 against all-255 rows give the
+    largest distances (L2^2 = 128 * 255^2 = 8,323,200 < 2^24, still exact),
+    and -0.0 counts as the byte 0; ties across the 64-row LDS stages keep
+    the lower train index."""
+    from droplet_visual_odometry_amd import ops
+    rng = np.random.default_rng(7 + norm)
+    dq, dt = sift_like(rng, 300), sift_like(rng, 700)
+    dq[:10] = 0.0
+    dq[10:20] = 255.0
+    dq[20:30] = -0.0
+    dt[::2] = 255.0  # many equal far rows; ties straddle LDS stages
+    dt[1::50] = 0.0
+    for k in (1, 2, 4):
+        i_g, d_g = ops.bf_knn_float(dq, dt, k, norm, ctx=gpu_ctx)
+        i_o, d_o = oracle_mod.bf_knn_float(dq, dt, k, norm)
+        np.testing.assert_array_equal(i_g, i_o)
+        np.testing.assert_array_equal(d_g.view(np.uint32), d_o.view(np.uint32))
