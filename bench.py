@@ -32,7 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-PMC_TRAFFIC = "r01g_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
+PMC_TRAFFIC = "r01i_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
 
 
 def parse():
