@@ -270,8 +270,8 @@ def chained_ate(fs, pool, corners, K, ref, B):
     import oracle
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     fs.reset_pose()
-    fs.process(pool[0:B + 1], fs.new_records(B), wait_torch=False)
-    _, T_abs = fs.pose_tail(corners[0:B], corners[1:B + 1], MARKER_LEN, wait_torch=False)
+    fs.process(pool[0:B + 1])  # fresh records: zero-filled on torch's stream, so the library waits for it
+    _, T_abs = fs.pose_tail(corners[0:B], corners[1:B + 1], MARKER_LEN)
     fs.sync()
     T_abs = T_abs.cpu().numpy()
     c = corners.cpu().numpy()

@@ -150,7 +150,7 @@ def _float_desc(d):
     return a
 
 
-def _knn_lists(q, t, k, norm):
+def _knn_lists(q, t, k, norm, sqrt_dist=False):
     if len(q) == 0 or len(t) == 0:
         return [[] for _ in range(len(q))] if len(t) == 0 else []
     if q.shape[1] != t.shape[1]:
@@ -159,6 +159,10 @@ def _knn_lists(q, t, k, norm):
         idx, dist = ops.bf_knn_float(q, t, k, norm)
     except DVOError as e:
         raise error(str(e)) from e
+    if sqrt_dist:
+        # FlannBasedMatcher::convertToDMatches: float FLANN distances (squared L2)
+        # become std::sqrt(float) in DMatch.distance; ranking stays on the squares
+        dist = np.sqrt(dist.astype(np.float32))
     out = []
     for qi in range(len(q)):
         row = []
@@ -226,7 +230,10 @@ class FlannBasedMatcher:
     distance (squared L2): FLANN's randomized kd-trees return the same
     neighbours whenever their approximate search finds the true ones; where it
     misses (seed dependent in OpenCV) the results differ — a documented
-    deviation (DESIGN.md row f)."""
+    deviation (DESIGN.md row f).  DMatch.distance is sqrt(float32) of the
+    squared distance, as OpenCV's FlannBasedMatcher::convertToDMatches does
+    for float descriptors, so the 0.75 ratio test (v3:227) compares distances,
+    not their squares."""
 
     def __init__(self, indexParams=None, searchParams=None):
         self.indexParams = dict(indexParams or {})
@@ -235,7 +242,8 @@ class FlannBasedMatcher:
     def knnMatch(self, queryDescriptors, trainDescriptors, k, mask=None, compactResult=False):
         if mask is not None:
             raise error("match masks are not supported")
-        out = _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), int(k), ops.NORM_L2SQR)
+        out = _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), int(k), ops.NORM_L2SQR,
+                         sqrt_dist=True)
         return [r for r in out if r] if compactResult else out
 
 

@@ -61,8 +61,13 @@ class FrameStream:
             raise ValueError("frames rows must be contiguous")
         if records is None:
             records = self.new_records(n - 1)
+            wait_torch = True  # the zero-fill runs on torch's stream: order the library's writes after it
         if wait_torch:
             self._after_torch()
+        # the caching allocator must not hand these blocks out again while the
+        # library's stream still reads the frames / writes the records
+        frames.record_stream(self._ext)
+        records.record_stream(self._ext)
         if undistort is not None:  # ops.Undistorter: frames are remapped into the stream's slab first
             self.ctx.check(self.ctx.lib.dvo_stream_process_undistorted(
                 self.h, undistort.h_, frames.data_ptr(), n, frames.stride(0), frames.stride(1),
@@ -103,12 +108,17 @@ class FrameStream:
         """Device pose tail for the last processed batch (see dvo.h); corners are
         float64 [pairs, k, 2] device tensors.  Returns (T_rel, T_abs) [pairs, 4, 4]."""
         pairs, k = corners_prev.shape[0], corners_prev.shape[1]
+        if T_rel is None or T_abs is None:
+            # blocks fresh from torch's stream may still be in use by work queued there
+            wait_torch = True
         if T_rel is None:
             T_rel = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
         if T_abs is None:
             T_abs = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
         if wait_torch:
             self._after_torch()
+        for t in (corners_prev, corners_cur, T_rel, T_abs):
+            t.record_stream(self._ext)
         self.ctx.check(self.ctx.lib.dvo_stream_pose_tail(self.h, corners_prev.data_ptr(), corners_cur.data_ptr(), k,
                                                          float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
         return T_rel, T_abs

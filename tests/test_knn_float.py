@@ -161,8 +161,14 @@ def test_cv_matchers_and_ratio_modes(gpu_ctx, oracle_mod):
     assert [p[0].queryIdx for p in passed] == expect and len(expect) >= 350
     i_f, d_f = oracle_mod.bf_knn_float(prev, cur, 2, 1)
     fl = cv.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50)).knnMatch(prev, cur, k=2)
+    # DMatch.distance = std::sqrt(float squared-L2), FlannBasedMatcher::convertToDMatches
+    s_f = np.sqrt(d_f.astype(np.float32))
     assert [(r[0].trainIdx, r[1].trainIdx, r[0].distance, r[1].distance) for r in fl] == \
-        [(int(a), int(b), float(c), float(d)) for (a, b), (c, d) in zip(i_f, d_f)]
+        [(int(a), int(b), float(c), float(d)) for (a, b), (c, d) in zip(i_f, s_f)]
+    fl_pass = [q for q, (m, n) in enumerate(fl) if m.distance < 0.75 * n.distance]
+    assert fl_pass == [q for q in range(600) if float(s_f[q, 0]) < 0.75 * float(s_f[q, 1])]
+    # the ratio on squared distances would be an effective 0.866 and pass more
+    assert len(fl_pass) < sum(float(d_f[q, 0]) < 0.75 * float(d_f[q, 1]) for q in range(600))
 
 
 @pytest.mark.gpu
@@ -190,6 +196,8 @@ def test_dropin_ratio_modes(gpu_ctx, oracle_mod, mode):
     me = types.SimpleNamespace(mode=mode, bf=cv.BFMatcher(normType=cv.NORM_L1, crossCheck=False))
     matches, top_prev, top_cur = v3.VisualOdometry.get_matches_between_two_frames(me, kp_prev, prev, kp_cur, cur)
     idx, dist = oracle_mod.bf_knn_float(prev, cur, 2, 1 if mode == "flann" else 0)
+    if mode == "flann":  # FLANN's DMatch.distance is sqrt(float) of the squared L2 distance
+        dist = np.sqrt(dist.astype(np.float32))
     keep = [q for q in range(300) if float(dist[q, 0]) < 0.75 * float(dist[q, 1])]
     assert len(matches) == 300 and len(keep) >= 150
     assert [kp.pt[0] for kp in top_prev] == [float(q) for q in keep]
