@@ -3,12 +3,15 @@
 
 Workload (BASELINE.json metric / configs[2]): a synthetic 1280x720 mono8
 stream, 2000 ORB features, one MI355X per rank.  One "step" is one batch of B
-new frames: the GPU runs ORB on B+1 device-resident frames (the first is the
-previous batch's last frame), Hamming cross-check matching, findEssentialMat
-(RANSAC, 5-point), recoverPose and the marker-scaled pose tail (triangulated
-marker corners -> scale -> 4x4 relative pose -> chained absolute pose) for the B
-consecutive pairs, and with N > 1 ranks all-gathers the B pair records over
-RCCL (the pose stream reassembly of SURVEY.md §8e).  value = (B x steps x ranks) / max-over-ranks wall time.
+new frames per rank: the GPU runs ORB on B+1 device-resident frames (the first
+is the previous batch's last frame), Hamming cross-check matching,
+findEssentialMat (RANSAC, 5-point), recoverPose and the marker-scaled pose tail
+(triangulated marker corners -> scale -> 4x4 relative pose -> chained absolute
+pose) for the B consecutive pairs.  With N > 1 ranks (configs[3]) ONE stream is
+sharded: each rank takes B consecutive pairs of a window of N x B plus a halo
+pair, the ranks all-gather records and relative poses over RCCL, and rank 0
+chains the window's absolute poses (main_sharded).
+value = (B x steps x ranks) / max-over-ranks wall time.
 
 Also reported:
   roofline      the dominant kernel group's algorithmic bytes / its HIP-event
@@ -102,9 +105,10 @@ def main():
 
     W, H, N, B = args.width, args.height, args.nfeatures, args.batch
     scene = SceneStream(W, H, device=str(dev))
+    if world > 1:
+        return main_sharded(args, world, rank, local_rank, backend, dev, scene)
     pool_n = args.pool or (2 * B + 1)
-    base = rank * 100_000  # each rank owns a disjoint stretch of the stream (weak scaling)
-    pool = torch.stack([scene.render(base + i) for i in range(pool_n)]).contiguous()
+    pool = torch.stack([scene.render(i) for i in range(pool_n)]).contiguous()
     torch.cuda.synchronize()
 
     ctx = Context(local_rank)
@@ -121,9 +125,6 @@ def main():
     T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     fss[0].reset_pose()
     torch.cuda.synchronize()
-    gdev = torch.device("cpu") if backend == "gloo" else dev
-    gathered = [torch.empty(world * recs_t[0].numel(), dtype=torch.uint8, device=gdev) for _ in range(S)] \
-        if world > 1 else None
     n_windows = max(1, (pool_n - 1) // B)
 
     def step(i):
@@ -132,14 +133,6 @@ def main():
         fs = fss[k]
         fs.process(pool[s:s + B + 1], recs_t[k], wait_torch=False)
         fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
-        if world > 1:
-            if backend == "gloo":
-                fs.sync()
-                dist.all_gather_into_tensor(gathered[k], recs_t[k].cpu())
-            else:
-                # RCCL (on torch's stream) reads the records once the library's stream has written them
-                torch.cuda.current_stream().wait_event(fs.record_event())
-                dist.all_gather_into_tensor(gathered[k], recs_t[k])
 
     def sync_all():
         for f in fss:
@@ -152,20 +145,12 @@ def main():
     if not args.no_profile:
         for f in fss:
             f.set_profiling(True)
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     sync_all()
-    if world > 1:
-        dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     recs = FrameStream.records_numpy(recs_t[(args.warmup + args.steps - 1) % S], B)
     stage_ms, calls = {}, 0
@@ -175,14 +160,8 @@ def main():
             calls += c
             for kk, v in sm.items():
                 stage_ms[kk] = stage_ms.get(kk, 0.0) + v
-    frames_total = B * args.steps * world
-    value = frames_total / elapsed
+    value = B * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
 
     m_avg = float(np.mean(recs["n_matches"])) if len(recs) else N / 2
     ok = int(np.sum(recs["status"] == 0))
@@ -203,12 +182,12 @@ def main():
                     "kernel_ms_per_launch": round(per_call[dom], 4),
                     "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
                     "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
-                    "path_frac": round(value / world * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9
+                    "path_frac": round(value * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9
                                        / HBM_PEAK_GBS, 8)}
 
     cpu = None
     pose_check = None
-    if args.cpu_seconds > 0 and world == 1:
+    if args.cpu_seconds > 0:
         cpu, ref = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds)
         # the same pairs on the GPU (window 0), compared with the oracle's R, t
         fss[0].process(pool[0:B + 1], recs_t[0], wait_torch=False)
@@ -248,9 +227,7 @@ def main():
         "data": "synthetic (seeded ray-cast textured room, droplet_visual_odometry_amd/synth.py)",
         "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, batch {B} new frames/step per GPU",
                    "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
-                   "parallelism": f"frame-sharded x{world}" + (
-                       (" + RCCL all_gather" if backend != "gloo" else " + gloo all_gather (rehearsal)")
-                       if world > 1 else ""),
+                   "parallelism": "single GPU",
                    "streams_in_flight": S,
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},
@@ -259,8 +236,116 @@ def main():
         "pose_check": pose_check,
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+
+
+def main_sharded(args, world, rank, local_rank, backend, dev, scene):
+    """N > 1 (BASELINE configs[3]): ONE stream sharded across the ranks.  A step
+    is a window of world x B consecutive pairs; rank r computes pairs
+    [r B, (r+1) B) of it plus the halo pair before them (dist.shard_window),
+    the ranks all-gather their 256-B records and T_rel rows over RCCL
+    (dist.ShardedPoseStream), and rank 0 chains the window's absolute poses on
+    the device (stream.PoseChain), continuing the chain across steps.  Weak
+    scaling: B new pairs per rank per step; value = world x B x steps / time."""
+    import torch
+    import torch.distributed as dist
+    from droplet_visual_odometry_amd import dist as ddist
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE, Context
+    from droplet_visual_odometry_amd.stream import FrameStream, PoseChain
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    W, H, N, B = args.width, args.height, args.nfeatures, args.batch
+    WP = world * B
+    n_windows = 2
+    wins = [ddist.shard_window(WP, world, rank, j * WP) for j in range(n_windows)]
+    # each rank renders only the frames of its own runs (no scatter)
+    pools = [torch.stack([scene.render(g) for g in range(f0, f1)]).contiguous() for (_, _, f0, f1, _) in wins]
+    corners = [torch.tensor(np.stack([scene.marker_corners(g) for g in range(f0, f1)]), dtype=torch.float64,
+                            device=dev) for (_, _, f0, f1, _) in wins]
+    torch.cuda.synchronize()
+    ctx = Context(local_rank)
+    S = max(1, args.streams)
+    host_gather = backend == "gloo"
+    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 2, max_iters=args.max_iters, ctx=ctx)
+           for _ in range(S)]
+    shs = [ddist.ShardedPoseStream(world, rank, WP, dev, host_gather=host_gather) for _ in range(S)]
+    recs_t = [f.new_records(B + 1) for f in fss]
+    T_rel = [torch.zeros((B + 1, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_loc = [torch.zeros((B + 1, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    for f in fss:
+        f.reset_pose()
+    chain = PoseChain(ctx) if rank == 0 else None
+    T_abs = [torch.empty((WP, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)] if rank == 0 else None
+    torch.cuda.synchronize()
+
+    def step(i):
+        j, k = i % n_windows, i % S
+        fs = fss[k]
+        fr, c = pools[j], corners[j]
+        halo = wins[j][4]
+        fs.process(fr, recs_t[k], wait_torch=False)
+        fs.pose_tail(c[:-1], c[1:], MARKER_LEN, T_rel[k], T_loc[k], wait_torch=False)
+        if host_gather:
+            fs.sync()
+        else:
+            # RCCL (on torch's stream) reads the records once the library's stream has written them
+            torch.cuda.current_stream().wait_event(fs.record_event())
+        _, all_T = shs[k].exchange(recs_t[k], T_rel[k], halo)
+        if rank == 0:
+            chain.run(all_T.to(dev, non_blocking=True) if host_gather else all_T, T_abs[k])
+
+    def sync_all():
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    sync_all()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    sync_all()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if host_gather else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    last = (args.warmup + args.steps - 1) % S
+    all_rec, _ = shs[last].exchange(recs_t[last], T_rel[last], wins[(args.warmup + args.steps - 1) % n_windows][4])
+    recs = all_rec.cpu().numpy().view(PAIR_RECORD_DTYPE)
+    value = WP * args.steps / elapsed
+    if rank == 0:
+        m_avg = float(np.mean(recs["n_matches"]))
+        out = {
+            "metric": ("frames/sec (detect+match+pose) at 1280\u00d7720, 2000 feats; ATE vs reference"
+                       if (W, H, N) == (1280, 720, 2000)
+                       else f"frames/sec (detect+match+pose) at {W}\u00d7{H}, {N} feats; ATE vs reference"),
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/f32/f64",
+            "data": "synthetic (seeded ray-cast textured room, droplet_visual_odometry_amd/synth.py)",
+            "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, one stream sharded over {world} "
+                                   f"ranks, {B} new frames/step per rank (+1 halo pair)",
+                       "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
+                       "parallelism": f"one stream pair-sharded x{world} + "
+                                      + ("gloo all_gather (rehearsal)" if host_gather else "RCCL all_gather")
+                                      + " of records and T_rel, rank-0 device pose chain",
+                       "streams_in_flight": S,
+                       "pairs_ok": f"{int(np.sum(recs['status'] == 0))}/{len(recs)}", "mean_matches": round(m_avg, 1),
+                       "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1)},
+            "roofline": None,
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
 
 
 def chained_ate(fs, pool, corners, K, ref, B):

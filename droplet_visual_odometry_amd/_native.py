@@ -101,6 +101,7 @@ _SIGNATURES = {
     "dvo_stream_process_undistorted": ([_vp, _vp, _vp, _c, _i64, _c, _vp], _c),
     "dvo_stream_share_pose": ([_vp, _vp], _c),
     "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
+    "dvo_pose_chain": ([_vp, _vp, _c, _vp, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),
     "dvo_stream_get_features": ([_vp, _c, _vp, _vp, _c, _ip], _c),
     "dvo_stream_get_matches": ([_vp, _c, _vp, _c, _ip], _c),

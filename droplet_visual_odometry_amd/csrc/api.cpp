@@ -510,6 +510,16 @@ int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const doub
     return DVO_OK;
 }
 
+int dvo_pose_chain(dvo_ctx* ctx, const double* d_T_rel, int n, double* d_T_carry, double* d_T_abs, void* hip_stream) {
+    if (!ctx) return DVO_EINVAL;
+    if (n < 0 || (n > 0 && (!d_T_rel || !d_T_carry || !d_T_abs)))
+        return fail(ctx, DVO_EINVAL, "pose chain needs T_rel, the carry and an output buffer");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(launch_pose_chain(d_T_rel, n, d_T_carry, d_T_abs,
+                              hip_stream ? (hipStream_t)hip_stream : ctx->stream));
+    return DVO_OK;
+}
+
 int dvo_stream_set_profiling(dvo_stream* s, int enable) {
     if (!s) return DVO_EINVAL;
     int rc = collect_events(s);

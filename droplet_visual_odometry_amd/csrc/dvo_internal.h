@@ -213,6 +213,10 @@ hipError_t launch_undistort_remap(const UndistortGeom& U, const int16_t* d_xy, c
 hipError_t launch_pose_tail(const double* Rt /*[pairs][12]*/, const int32_t* info /*[pairs][4]*/, int pairs,
                             const double* K, const double* cprev, const double* ccur, int k, double marker_length,
                             double* carry, double* T_rel, double* T_abs, hipStream_t s);
+// T_abs[p] = T_carry . T_rel[0] ... T_rel[p] in pair order (the pose_tail chain on
+// its own: the reassembled pose stream of a sharded run); T_carry is updated.
+hipError_t launch_pose_chain(const double* T_rel /*[n][16]*/, int n, double* T_carry /*16*/, double* T_abs,
+                             hipStream_t s);
 hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
 // Float-descriptor kNN (NORM_L1 / squared L2), dim 64 or 128, k 1..4, over
 // `ranges` = knn_ranges(nq, nt, CU count) train ranges; d_part / d_pidx hold

@@ -1629,7 +1629,8 @@ struct TailArgs {
     const double* ccur;
     int k;
     double L;
-    double* carry;
+    double* carry;   // P_prev carry (12 doubles); null for a chain-only launch
+    double* tcarry;  // T_abs carry (16 doubles): in = pose before the first pair, out = after the last
     double* T_rel;
     double* T_abs;
 };
@@ -1646,10 +1647,19 @@ __global__ void pose_tail_kernel(TailArgs a) {
     const double* Rt = a.Rt + (int64_t)p * 12;
     double Pc[12], Pp[12];
     proj_of(a.K, Rt, Pc);
-    if (p == 0) {
+    // P_prev is the projection of the last pair that got through (the reference
+    // sets previous_projection_matrix only at the end of a successful pair,
+    // v3:344); the carry when no earlier pair of this batch did.
+    int q = p - 1;
+    while (q >= 0) {
+        const int32_t* iq = a.info + (int64_t)q * 4;
+        if (iq[3] == DVO_OK && iq[0] == 3) break;
+        --q;
+    }
+    if (q < 0) {
         for (int r = 0; r < 12; ++r) Pp[r] = a.carry[r];
     } else {
-        proj_of(a.K, a.Rt + (int64_t)(p - 1) * 12, Pp);
+        proj_of(a.K, a.Rt + (int64_t)q * 12, Pp);
     }
     double X0[4], X1[4];
     const double* cp = a.cprev + (int64_t)p * a.k * 2;
@@ -1697,14 +1707,16 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
     __shared__ double tr[kChunk * 16];
     const int lane = threadIdx.x;
     int last_ok = -1;
-    for (int p = lane; p < a.pairs; p += 64) {
-        const int32_t* inf = a.info + (int64_t)p * 4;
-        if (inf[3] == DVO_OK && inf[0] == 3) last_ok = p;
-    }
+    if (a.info) {
+        for (int p = lane; p < a.pairs; p += 64) {
+            const int32_t* inf = a.info + (int64_t)p * 4;
+            if (inf[3] == DVO_OK && inf[0] == 3) last_ok = p;
+        }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
+        for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
+    }
     const int c = lane & 3;
-    double t = a.carry[12 + (lane & 15)];
+    double t = a.tcarry[lane & 15];
     for (int p0 = 0; p0 < a.pairs; p0 += kChunk) {
         const int n = min(kChunk, a.pairs - p0);
         __syncthreads();
@@ -1717,8 +1729,8 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
             if (lane < 16) a.T_abs[(int64_t)(p0 + q) * 16 + lane] = t;
         }
     }
-    if (lane < 16) a.carry[12 + lane] = t;
-    if (lane == 0 && last_ok >= 0) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
+    if (lane < 16) a.tcarry[lane] = t;
+    if (lane == 0 && last_ok >= 0 && a.carry) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
 }
 
 __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, int mp, int mi, int32_t* out) {
@@ -1789,9 +1801,21 @@ hipError_t launch_pose_tail(const double* Rt, const int32_t* info, int pairs, co
     a.k = k;
     a.L = marker_length;
     a.carry = carry;
+    a.tcarry = carry + 12;
     a.T_rel = T_rel;
     a.T_abs = T_abs;
     hipLaunchKernelGGL(pose_tail_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(pose_chain_kernel, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pose_chain(const double* T_rel, int n, double* T_carry, double* T_abs, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    TailArgs a{};
+    a.pairs = n;
+    a.tcarry = T_carry;
+    a.T_rel = const_cast<double*>(T_rel);
+    a.T_abs = T_abs;
     hipLaunchKernelGGL(pose_chain_kernel, dim3(1), dim3(64), 0, s, a);
     return hipGetLastError();
 }

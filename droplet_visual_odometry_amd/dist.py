@@ -9,14 +9,20 @@ collective: after the batch each rank holds its 256-byte pair records and the
 only exchange is one all-gather of those records (RCCL over xGMI on the GPU,
 gloo in the CPU tests) to reassemble the pose stream in order.
 
-The absolute pose chain T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) is a prefix
-product; ranks chain their own run from identity and `compose_chain` folds the
-per-rank partial products in rank order — equal to the sequential chain up to
-floating-point reassociation of the 4x4 products (pinned in tests/test_dist.py).
-The marker-scale step also needs the previous pair's projection matrix
-(v3:343): with `shard_frames(..., left_halo=True)` a rank also loads frame
-p0-1 and computes pair p0-1, whose R|t gives its first pair's P_prev through
-the device carry; that extra pair's record is dropped before the gather.
+The marker-scale step of pair p needs the previous pair's projection matrix
+P = K [R | t] (v3:264-265, :344).  So a rank whose run starts at p0 > 0 also
+loads frame p0-1 (the left halo, `shard_window`) and computes pair p0-1: its
+R|t is P_prev for p0, exactly as on one rank, and its record and T_rel are
+dropped before the exchange.  (On one rank P_prev is the last *successful*
+pair's; the halo reproduces that whenever the halo pair itself succeeds, i.e.
+unless frame p0-1 or p0 has no features.)
+
+`ShardedPoseStream.exchange` all-gathers every rank's records and T_rel rows in
+pair order; rank 0 then chains T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) over
+the whole window on the device (`stream.PoseChain`, the same left-to-right
+4x4 arithmetic as the single-rank pose tail, so T_abs is bit-identical).  The
+host helpers `local_chain` / `compose_chain` fold per-rank partial products
+instead (equal up to reassociation, tests/test_dist.py).
 """
 from __future__ import annotations
 
@@ -44,6 +50,66 @@ def shard_frames(n_frames: int, world: int, rank: int, left_halo: bool = False) 
 
 def max_pairs_per_rank(n_frames: int, world: int) -> int:
     return max(p1 - p0 for p0, p1 in (shard_pairs(n_frames, world, r) for r in range(world)))
+
+
+def shard_window(n_pairs: int, world: int, rank: int, first_pair: int = 0):
+    """`rank`'s share of a window of `n_pairs` consecutive pairs of ONE stream
+    starting at global pair `first_pair`: (p0, p1, f0, f1, halo) -- pairs
+    [p0, p1), frames [f0, f1) to load (pair p is frames p, p+1) and halo = 1
+    when frame p0-1 is loaded too, so that the rank's first computed pair is
+    the dropped halo pair p0-1."""
+    a, b = shard_pairs(n_pairs + 1, world, rank)
+    p0, p1 = first_pair + a, first_pair + b
+    if p1 <= p0:
+        return p0, p0, p0, p0, 0
+    halo = 1 if p0 > 0 else 0
+    return p0, p1, p0 - halo, p1 + 1, halo
+
+
+class ShardedPoseStream:
+    """The exchange step of one pose stream sharded across ranks (SURVEY.md
+    §8e, BASELINE configs[3]): windows of `window_pairs` pairs, each rank
+    computing its `shard_window` run (halo pair first) on its own GPU.
+
+    `exchange(records, T_rel, halo)` takes the rank's computed records
+    (uint8, 256 B per pair, halo pair first) and T_rel ([pairs, 4, 4] float64)
+    and returns the window's records and T_rel in global pair order on every
+    rank: one all-gather each (RCCL over xGMI; gloo through host memory with
+    host_gather=True).  Inputs are sliced in place, so the gathered sends are
+    the rank's buffers themselves: they must hold at least halo + cap pairs,
+    cap = max pairs per rank.  The returned tensors are views of the receive
+    buffers (no copy when the shards are equal), valid until the next exchange."""
+
+    def __init__(self, world: int, rank: int, window_pairs: int, device, group=None, host_gather: bool = False):
+        import torch
+        from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+        self.world, self.rank, self.window_pairs, self.group = world, rank, window_pairs, group
+        self.rb = PAIR_RECORD_DTYPE.itemsize
+        self.counts = [b - a for a, b in (shard_pairs(window_pairs + 1, world, r) for r in range(world))]
+        self.cap = max(self.counts)
+        self.n_local = self.counts[rank]
+        self.host_gather = host_gather
+        gdev = torch.device("cpu") if host_gather else torch.device(device)
+        self.recv_rec = torch.empty(world * self.cap * self.rb, dtype=torch.uint8, device=gdev)
+        self.recv_T = torch.empty((world * self.cap, 4, 4), dtype=torch.float64, device=gdev)
+
+    def exchange(self, records, T_rel, halo: int):
+        import torch.distributed as dist
+        rb, cap = self.rb, self.cap
+        if records.numel() < (halo + cap) * rb or T_rel.shape[0] < halo + cap:
+            raise ValueError(f"buffers must hold halo + {cap} pairs")
+        send_rec = records[halo * rb:(halo + cap) * rb]
+        send_T = T_rel[halo:halo + cap]
+        if self.host_gather:
+            send_rec, send_T = send_rec.cpu(), send_T.cpu()
+        dist.all_gather_into_tensor(self.recv_rec, send_rec, group=self.group)
+        dist.all_gather_into_tensor(self.recv_T.view(-1), send_T.reshape(-1), group=self.group)
+        if all(c == cap for c in self.counts):
+            return self.recv_rec, self.recv_T
+        import torch
+        recs = torch.cat([self.recv_rec[r * cap * rb:(r * cap + c) * rb] for r, c in enumerate(self.counts)])
+        Ts = torch.cat([self.recv_T[r * cap:r * cap + c] for r, c in enumerate(self.counts)])
+        return recs, Ts
 
 
 def gather_records(records, n_local: int, n_frames: int, group=None):

@@ -9,6 +9,7 @@ only containers for device memory; all compute is in libdvo_hip.so.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 
 import numpy as np
@@ -37,6 +38,7 @@ class FrameStream:
         self.ctx.check(self.ctx.lib.dvo_stream_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
         self._ext = torch.cuda.ExternalStream(self.hip_stream, device=self.device)
+        self._held = collections.deque()  # (event, tensors) in flight on the library's stream
         self.width, self.height, self.max_frames, self.nfeatures = width, height, max_frames, nfeatures
         self.K = K.reshape(3, 3)
 
@@ -64,18 +66,26 @@ class FrameStream:
             wait_torch = True  # the zero-fill runs on torch's stream: order the library's writes after it
         if wait_torch:
             self._after_torch()
-        # the caching allocator must not hand these blocks out again while the
-        # library's stream still reads the frames / writes the records
-        frames.record_stream(self._ext)
-        records.record_stream(self._ext)
         if undistort is not None:  # ops.Undistorter: frames are remapped into the stream's slab first
             self.ctx.check(self.ctx.lib.dvo_stream_process_undistorted(
                 self.h, undistort.h_, frames.data_ptr(), n, frames.stride(0), frames.stride(1),
                 records.data_ptr() if n > 1 else None))
-            return records
-        self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
-                                                       frames.stride(1), records.data_ptr() if n > 1 else None))
+        else:
+            self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
+                                                           frames.stride(1), records.data_ptr() if n > 1 else None))
+        self._hold(frames, records)
         return records
+
+    def _hold(self, *tensors):
+        """Keep the tensors the library's stream reads or writes alive until that
+        work has finished, so torch's caching allocator cannot hand their blocks
+        to a new tensor meanwhile.  (Not record_stream: the allocator would then
+        record events on this stream after close() destroyed it.)"""
+        ev = torch.cuda.Event()
+        ev.record(self._ext)
+        self._held.append((ev, tensors))
+        while self._held and self._held[0][0].query():
+            self._held.popleft()
 
     def _after_torch(self):
         """Order the library's HIP stream after work already queued on torch's
@@ -117,10 +127,9 @@ class FrameStream:
             T_abs = torch.empty((pairs, 4, 4), dtype=torch.float64, device=self.device)
         if wait_torch:
             self._after_torch()
-        for t in (corners_prev, corners_cur, T_rel, T_abs):
-            t.record_stream(self._ext)
         self.ctx.check(self.ctx.lib.dvo_stream_pose_tail(self.h, corners_prev.data_ptr(), corners_cur.data_ptr(), k,
                                                          float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
+        self._hold(corners_prev, corners_cur, T_rel, T_abs)
         return T_rel, T_abs
 
     def set_profiling(self, enable: bool = True):
@@ -136,6 +145,7 @@ class FrameStream:
 
     def sync(self):
         self.ctx.check(self.ctx.lib.dvo_stream_sync(self.h))
+        self._held.clear()
 
     @staticmethod
     def records_numpy(records: torch.Tensor, n_pairs: int) -> np.ndarray:
@@ -166,11 +176,44 @@ class FrameStream:
 
     def close(self):
         if getattr(self, "h", None):
-            self.ctx.lib.dvo_stream_destroy(self.h)
+            self.ctx.lib.dvo_stream_destroy(self.h)  # synchronises the stream first
             self.h = None
+            if getattr(self, "_held", None):
+                self._held.clear()
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+class PoseChain:
+    """Absolute-pose chain T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) on the
+    device (dvo_pose_chain) with a persistent carry: the reassembly step of a
+    sharded pose stream (dist.ShardedPoseStream).  Runs on torch's current
+    stream, where the all-gather that produced T_rel ran."""
+
+    def __init__(self, ctx: Context | None = None, device: int | None = None, T0=None):
+        self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
+        self.device = torch.device("cuda", self.ctx.device)
+        self.carry = torch.empty(16, dtype=torch.float64, device=self.device)
+        self.reset(T0)
+
+    def reset(self, T0=None):
+        T0 = np.eye(4) if T0 is None else np.asarray(T0, np.float64)
+        self.carry.copy_(torch.from_numpy(np.ascontiguousarray(T0).reshape(16)))
+
+    def run(self, T_rel: torch.Tensor, T_abs: torch.Tensor | None = None) -> torch.Tensor:
+        if T_rel.dtype != torch.float64 or not T_rel.is_cuda or not T_rel.is_contiguous():
+            raise ValueError("T_rel must be a contiguous float64 [n, 4, 4] device tensor")
+        n = T_rel.shape[0]
+        if T_abs is None:
+            T_abs = torch.empty((n, 4, 4), dtype=torch.float64, device=self.device)
+        if T_abs.shape[0] < n or not T_abs.is_contiguous():
+            raise ValueError("T_abs must be a contiguous float64 [>= n, 4, 4] device tensor")
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        self.ctx.check(self.ctx.lib.dvo_pose_chain(self.ctx.h, T_rel.data_ptr(), n, self.carry.data_ptr(),
+                                                   T_abs.data_ptr(), st))
+        return T_abs
+

@@ -195,6 +195,16 @@ int dvo_stream_share_pose(dvo_stream* s, dvo_stream* owner);
 int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
                          double marker_length, double* d_T_rel, double* d_T_abs);
 
+/* The absolute-pose chain of previous_current_matching (v3:367,
+ * T_robot_cur = T_robot_prev . T_prev->cur) on its own, for pose streams
+ * reassembled from sharded runs: rank 0 all-gathers every
+ * rank's T_rel and chains them in pair order with the same arithmetic as
+ * dvo_stream_pose_tail, so the result is bit-identical to one rank chaining the
+ * whole stream.  d_T_rel: device [n][16]; d_T_carry: device 16 doubles, the pose
+ * before the first pair on entry and after the last on return; d_T_abs: device
+ * [n][16].  Asynchronous on hip_stream (NULL = the context's stream). */
+int dvo_pose_chain(dvo_ctx* ctx, const double* d_T_rel, int n, double* d_T_carry, double* d_T_abs, void* hip_stream);
+
 /* Per-stage device time via HIP events recorded on the stream's HIP stream
  * around each kernel group (0 pyramid, 1 blur, 2 fast, 3 select+harris,
  * 4 describe, 5 match, 6 ransac, 7 recoverPose+records, 8 pose tail).  Accumulated over

@@ -250,7 +250,7 @@ def pair_pose(img_prev, img_cur, K, nfeatures=500, max_iters=1000, kp_prev=None)
     p1 = keypoints_to_points(kp1[q]).astype(np.float64)
     p2 = keypoints_to_points(kp2[t]).astype(np.float64)
     E, mask, iters = find_essential(p1, p2, K, max_iters=max_iters)
-    out = dict(kp_prev=kp1, kp_cur=kp2, desc_cur=d2, q=q, t=t, p1=p1, p2=p2, E=E, iters=iters)
+    out = dict(kp_prev=kp1, kp_cur=kp2, desc_cur=d2, q=q, t=t, p1=p1, p2=p2, E=E, mask=mask, iters=iters)
     if E is None or E.shape[0] != 3:
         out.update(R=None, t_unit=None, good=0)
         return out

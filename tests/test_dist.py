@@ -86,3 +86,105 @@ def test_gather_records_gloo_world2(n_frames):
         assert tx == [0.5 * i for i in range(n_frames - 1)]
         want = [0 if i < ddist.shard_pairs(n_frames, 2, 0)[1] else 1 for i in range(n_frames - 1)]
         assert st == want
+
+
+@pytest.mark.parametrize("n_pairs,world", [(8, 2), (7, 2), (5, 3)])
+def test_shard_window_one_stream(n_pairs, world):
+    """Each window pair is computed by exactly one rank; every rank but the one
+    holding the stream's first pair loads one halo frame before its run."""
+    for first in (0, n_pairs):
+        seen = []
+        for r in range(world):
+            p0, p1, f0, f1, halo = ddist.shard_window(n_pairs, world, r, first)
+            seen.extend(range(p0, p1))
+            if p1 > p0:
+                assert (f0, f1) == (p0 - halo, p1 + 1)
+                assert halo == (0 if p0 == 0 else 1)
+        assert seen == list(range(first, first + n_pairs))
+
+
+def _oracle_records(frames, K, n, P0, corners, marker_len):
+    """Records + T_rel of consecutive pairs from the oracle (the CPU restatement
+    of what FrameStream.process + pose_tail compute), P_prev carried from P0."""
+    import oracle
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+    pairs = len(frames) - 1
+    rec = np.zeros(pairs, PAIR_RECORD_DTYPE)
+    T_rel = np.zeros((pairs, 4, 4))
+    kp_prev = None
+    P, T = P0, np.eye(4)
+    for i in range(pairs):
+        r = oracle.pair_pose(frames[i], frames[i + 1], K, n, kp_prev=kp_prev)
+        kp_prev = (r["kp_cur"], r["desc_cur"])
+        rec["R"][i] = r["R"].ravel()
+        rec["t"][i] = r["t_unit"].ravel()
+        rec["E"][i] = r["E"].ravel()
+        rec["n_matches"][i] = len(r["q"])
+        rec["ransac_iters"][i] = r["iters"]
+        P, T_rel[i], T = oracle.pose_tail(K, r["R"], r["t_unit"], corners[i], corners[i + 1], marker_len, P, T)
+    return rec, T_rel
+
+
+def _sharded_worker(rank, world, port, n_pairs, windows, out):
+    import sys
+    import torch
+    import torch.distributed as dist
+    torch.set_num_threads(2)  # two ranks on 8 host cores: oversubscribed torch threads make rendering ~50x slower
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = ddist.ShardedPoseStream(world, rank, n_pairs, "cpu")
+    rb = PAIR_RECORD_DTYPE.itemsize
+    T = np.eye(4)
+    got_rec, got_T = [], []
+    for w in range(windows):
+        p0, p1, f0, f1, halo = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
+        frames, K = synth_frames(320, 240, range(f0, f1))
+        corners = np.stack([marker_corners(i, K) for i in range(f0, f1)])
+        rec, T_rel = _oracle_records(frames, K, 300, K @ np.hstack((np.eye(3), np.zeros((3, 1)))), corners,
+                                     MARKER_LEN)
+        recs = np.zeros(sh.cap + 1, PAIR_RECORD_DTYPE)
+        recs[:len(rec)] = rec
+        Ts = np.zeros((sh.cap + 1, 4, 4))
+        Ts[:len(T_rel)] = T_rel
+        all_rec, all_T = sh.exchange(torch.from_numpy(recs.view(np.uint8).copy()), torch.from_numpy(Ts), halo)
+        assert all_rec.numel() == n_pairs * rb and all_T.shape[0] == n_pairs
+        for M in all_T.numpy():          # rank 0's chain, sequential as on one rank
+            T = T.dot(M)
+            got_T.append(T)
+        got_rec.append(all_rec.numpy().view(PAIR_RECORD_DTYPE).copy())  # views of the recv buffers
+    out[rank] = (np.concatenate(got_rec).tobytes(), np.stack(got_T).tobytes())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_pairs,windows", [(4, 2), (5, 1)])
+def test_sharded_one_stream_matches_single_rank_gloo(oracle_mod, n_pairs, windows):
+    """One stream sharded over 2 ranks with the left halo: the exchanged records
+    (R, t, E, counts) and the chained T_abs equal a single rank's sequential run
+    over the same frames, bit for bit (C4, trajectory_evaluation_dual_process.py:172-252)."""
+    import torch.multiprocessing as mp
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sharded_worker, args=(2, _free_port(), n_pairs, windows, out), nprocs=2, join=True)
+    F = n_pairs * windows + 1
+    frames, K = synth_frames(320, 240, range(F))
+    corners = np.stack([marker_corners(i, K) for i in range(F)])
+    rec, T_rel = _oracle_records(frames, K, 300, K @ np.hstack((np.eye(3), np.zeros((3, 1)))), corners, MARKER_LEN)
+    T = np.eye(4)
+    want_T = []
+    for M in T_rel:
+        T = T.dot(M)
+        want_T.append(T)
+    for r in range(2):
+        got_rec, got_T = out[r]
+        got = np.frombuffer(got_rec, PAIR_RECORD_DTYPE)
+        assert got.tobytes() == rec.tobytes()
+        np.testing.assert_array_equal(np.frombuffer(got_T).reshape(-1, 4, 4), np.stack(want_T))
