@@ -16,8 +16,9 @@ value = (B x steps x ranks) / max-over-ranks wall time.
 Also reported:
   roofline      the dominant kernel group's algorithmic bytes / its HIP-event
                 time on the library's stream, against 8 TB/s HBM
-  cpu_baseline  the oracle (C++ restatement of the OpenCV path) on one host
-                core over a bounded sample of the same stream (rank 0, N=1)
+  cpu_baseline  the oracle (C++ restatement of the OpenCV path, -O3
+                -march=native) over bounded samples of the same stream on all
+                host threads (value) and on one core (rank 0, N=1)
 
 Run: python bench.py --gpus N --steps K --warmup W
 """
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=0, help="distinct frames rendered per rank (default 2*batch+1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP-event timing")
+    ap.add_argument("--dropin-seconds", type=float, default=4.0,
+                    help="bounded timing of the per-pair drop-in surface (0 = skip)")
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight: each on its own dvo_stream / HIP stream, so one batch's "
                          "serial RANSAC tail overlaps the next batch's ORB")
@@ -119,7 +122,7 @@ def main():
         f.share_pose(fss[0])  # one pose stream across the alternating batches
     recs_t = [f.new_records(B) for f in fss]
     from droplet_visual_odometry_amd.synth import MARKER_LEN
-    corners = torch.tensor(np.stack([scene.marker_corners(base + i) for i in range(pool_n)]), dtype=torch.float64,
+    corners = torch.tensor(np.stack([scene.marker_corners(i) for i in range(pool_n)]), dtype=torch.float64,
                            device=dev)
     T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
@@ -210,6 +213,8 @@ def main():
                       "ate_m": ate, "reference": "oracle/ C++ restatement, same frames; ATE = RMS position "
                                                  "difference of the marker-scaled chained trajectories"}
 
+    dropin = dropin_rate(pool, corners, scene.K, N, args.dropin_seconds) if args.dropin_seconds > 0 else None
+
     default_cfg = (W, H, N) == (1280, 720, 2000)
     out = {
         "metric": ("frames/sec (detect+match+pose) at 1280\u00d7720, 2000 feats; ATE vs reference" if default_cfg
@@ -234,6 +239,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "pose_check": pose_check,
+        "dropin": dropin,
     }
     print(json.dumps(out), flush=True)
 
@@ -391,29 +397,124 @@ def pmc_traffic(kernel, W, H, N, B):
     return round((k["fetch_bytes"] + k["write_bytes"]) * scale), src
 
 
+def dropin_rate(pool, corners, K, nfeatures, seconds, n_frames=48):
+    """Pairs/s of the drop-in surface the ROS harness calls: the drop-in
+    VisualOdometry.visual_odometry_calculations (visual_odometry_v3.py:384-408)
+    one pair at a time, host mono8 frames in and 4x4 poses out, synchronous,
+    chained as trajectory_evaluation_dual_process.py:151-166 does (previous
+    absolute pose and both frames' marker corners per call).  ORB runs at the
+    bench's nfeatures (the reference's ORB_create() default is 500)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "droplet_visual_odometry_amd", "dropin"))
+    try:
+        import visual_odometry_v3 as v3
+    finally:
+        sys.path.pop(0)
+    d = ", ".join(repr(float(v)) for v in np.asarray(K).ravel())
+    with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as fh:
+        fh.write(f"camera_matrix:\n  rows: 3\n  cols: 3\n  data: [{d}]\n"
+                 "distortion_coefficients:\n  rows: 1\n  cols: 5\n  data: [0.0, 0.0, 0.0, 0.0, 0.0]\n")
+        cal = fh.name
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    vo = v3.VisualOdometry(mode="orb", calibration_file_path=cal, controlled=True, real_marker_length=MARKER_LEN)
+    os.unlink(cal)
+    vo.feature_detector.setMaxFeatures(nfeatures)
+    n = min(n_frames, len(pool))
+    frames = [pool[i].cpu().numpy() for i in range(n)]
+    cs = corners[:n].cpu().numpy()
+    T = vo.robot_curr_position
+    T, _ = vo.visual_odometry_calculations(frames[0], frames[1], T, cs[0], cs[1])  # warm-up (plans, scratch)
+    lat = []
+    t0 = time.perf_counter()
+    i = 1
+    while time.perf_counter() - t0 < seconds:
+        a = i % (n - 1)
+        t1 = time.perf_counter()
+        T, _ = vo.visual_odometry_calculations(frames[a], frames[a + 1], T, cs[a], cs[a + 1])
+        lat.append(time.perf_counter() - t1)
+        i += 1
+    dt = time.perf_counter() - t0
+    lat = np.array(lat) * 1e3
+    return {"dropin_pairs_per_s": round(len(lat) / dt, 2), "ms_per_pair_median": round(float(np.median(lat)), 3),
+            "ms_per_pair_p90": round(float(np.percentile(lat, 90)), 3), "pairs": len(lat),
+            "surface": "dropin/visual_odometry_v3.VisualOdometry.visual_odometry_calculations, one synchronous call "
+                       "per pair (host frames in, poses out), as trajectory_evaluation_dual_process.py:151-166"}
+
+
+def cpu_threads():
+    """Host threads for the all-cores leg: the CPUs this process may run on,
+    capped by OMP_NUM_THREADS (the GPU box sets it to the box's CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
-    """The oracle (restated OpenCV path, -O2 C++, one core) on the same stream:
-    sequential pairs with the previous frame's features reused (streaming mode)."""
+    """The oracle (restated OpenCV path, C++ built -O3 -march=native for this
+    host) on the same stream, in streaming mode (each frame detected once,
+    its features reused by the next pair):
+      single core   sequential pairs, the reference's execution model
+                    (trajectory_evaluation_dual_process.py:172);
+      all cores     the stream split into contiguous runs, one per thread
+                    (ctypes releases the GIL inside the C++ calls), each run
+                    sequential with feature reuse -- SURVEY.md §8d (2).
+    Each leg runs about `seconds`.  value = the all-cores figure."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    oracle.build()
+    lib_path = oracle.use_native_build()
+    model, _ = oracle.host_cpu()
+    host = lambda i: pool[i].cpu().numpy()  # noqa: E731
+
     t0 = time.perf_counter()
-    kp_prev = oracle.detect_and_compute(pool[0].cpu().numpy(), nfeatures)
-    n = 0
+    kp_prev = oracle.detect_and_compute(host(0), nfeatures)
     i = 0
     ref = []
     while time.perf_counter() - t0 < seconds and i + 1 < len(pool):
-        a, b = pool[i].cpu().numpy(), pool[i + 1].cpu().numpy()
-        r = oracle.pair_pose(a, b, K, nfeatures, max_iters=max_iters, kp_prev=kp_prev)
+        r = oracle.pair_pose(host(i), host(i + 1), K, nfeatures, max_iters=max_iters, kp_prev=kp_prev)
         kp_prev = (r["kp_cur"], r["desc_cur"])
         ref.append((r["R"], r["t_unit"]))
-        n += 1
         i += 1
-    dt = time.perf_counter() - t0
-    return ({"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-             "sample": f"{n} consecutive pairs of the same {pool.shape[2]}x{pool.shape[1]} stream ({dt:.1f} s, "
-                       f"first frame's detect included), oracle/ C++ restatement of the OpenCV path, streaming "
-                       f"mode, one host core"}, ref)
+    dt1 = time.perf_counter() - t0
+    n1 = i
+
+    T = cpu_threads()
+    run = max(2, (len(pool) - 1) // T)
+    done = [0] * T
+    deadline = time.perf_counter() + seconds
+
+    def worker(t):
+        a = t * run
+        if a + 1 >= len(pool):
+            return
+        kp = oracle.detect_and_compute(host(a), nfeatures)
+        j = a
+        while j + 1 < min(len(pool), a + run + 1) and time.perf_counter() < deadline:
+            r = oracle.pair_pose(host(j), host(j + 1), K, nfeatures, max_iters=max_iters, kp_prev=kp)
+            kp = (r["kp_cur"], r["desc_cur"])
+            done[t] += 1
+            j += 1
+
+    t1 = time.perf_counter()
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dtn = time.perf_counter() - t1
+    nn = sum(done)
+    W, H = pool.shape[2], pool.shape[1]
+    return ({"value": round(nn / dtn, 3), "unit": "frames/s", "cores": T, "kind": "port",
+             "sample": f"{nn} pairs of the same {W}x{H} stream in {dtn:.1f} s on {T} threads (the stream split into "
+                       f"{T} contiguous runs, each sequential with feature reuse; each run's first detect included); "
+                       f"oracle/ C++ restatement of the OpenCV path built -O3 -march=native "
+                       f"({os.path.basename(lib_path)})",
+             "single_core": {"value": round(n1 / dt1, 3), "cores": 1,
+                             "sample": f"{n1} consecutive pairs in {dt1:.1f} s, first frame's detect included"},
+             "host_cpus": os.cpu_count(), "cpu_model": model}, ref)
 
 
 if __name__ == "__main__":

@@ -681,13 +681,14 @@ int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t*
     void *bq, *bt, *bnn, *bout, *bm;
     int rc;
     if ((rc = scratch(ctx, 0, (size_t)nq * 32, &bq)) || (rc = scratch(ctx, 1, (size_t)nt * 32, &bt)) ||
-        (rc = scratch(ctx, 2, (size_t)(nq + nt) * 4, &bnn)) || (rc = scratch(ctx, 3, (size_t)nq * sizeof(dvo_dmatch), &bout)) ||
+        (rc = scratch(ctx, 2, match_pair_work_size(nq, nt), &bnn)) ||
+        (rc = scratch(ctx, 3, (size_t)nq * sizeof(dvo_dmatch), &bout)) ||
         (rc = scratch(ctx, 4, 64, &bm)))
         return rc;
     HIP_TRY(hipMemcpyAsync(bq, dq, (size_t)nq * 32, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(bt, dt, (size_t)nt * 32, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(launch_match_pair((const uint8_t*)bq, nq, (const uint8_t*)bt, nt, cross_check, (int32_t*)bnn,
-                              (dvo_dmatch*)bout, (int*)bm, ctx->stream));
+    HIP_TRY(launch_match_pair((const uint8_t*)bq, nq, (const uint8_t*)bt, nt, cross_check, bnn, (dvo_dmatch*)bout,
+                              (int*)bm, ctx->stream));
     int m = 0;
     HIP_TRY(hipMemcpyAsync(&m, bm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

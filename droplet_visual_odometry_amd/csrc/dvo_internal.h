@@ -227,7 +227,10 @@ size_t knn_bytes_size(int nq, int nt, int dim);
 hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, int dim, int k, int norm, int ranges,
                             void* d_bytes, float* d_part, int32_t* d_pidx, float* d_dist, int32_t* d_idx,
                             hipStream_t s);
-hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
+// One-pair Hamming match (dvo_bf_match_hamming) on the stream's MFMA matcher;
+// d_work: match_pair_work_size(nq, nt) bytes.  Output in queryIdx order.
+size_t match_pair_work_size(int nq, int nt);
+hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
                                    int* d_k, hipStream_t s);

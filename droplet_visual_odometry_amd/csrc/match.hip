@@ -5,14 +5,10 @@
 // order is (distance, queryIdx)) and KeyPoint_convert of the matched keypoints
 // (v3:355, v3:358).
 //
-// nn_kernel: one workgroup = 512 queries x ALL trains.  The train descriptors
-// (<= kp_cap x 32 B) are staged once in LDS and read back as broadcast b128
-// loads; each thread keeps two query descriptors in registers and scans every
-// train with v_xor + v_bcnt (integer, 8 dwords), keeping a packed
-// (distance << 16 | index) minimum, which yields OpenCV's "first index at the
-// minimum distance" tie rule.  Forward (prev->cur) and backward (cur->prev)
-// directions run in the same launch (grid.y).
-// crosscheck_sort_kernel: mutual-NN filter, then a bitonic sort of the unique
+// nn_mfma_kernel: forward and backward nearest neighbours of a pair on the
+// matrix cores (int8 MFMA over +-1 descriptor bytes), for the batched stream
+// and, through a one-pair parameter block, for the per-call C-ABI.
+// crosscheck_*_kernel: mutual-NN filter, then a bitonic sort of the unique
 // keys (distance << 16 | queryIdx) in LDS, then the point gather.
 #include <algorithm>
 #include <cfloat>
@@ -22,170 +18,6 @@
 
 namespace dvo {
 namespace {
-
-constexpr int kNNThreads = 256;
-constexpr int kNNPerThread = 2;
-constexpr int kNNQ = kNNThreads * kNNPerThread;
-
-struct NNJob {
-    const uint8_t* q;
-    int nq;
-    const uint8_t* t;
-    int nt;
-    int32_t* out;
-};
-
-constexpr int kTrainChunk = 2048;   // trains staged per LDS fill (64 KB)
-
-__device__ __forceinline__ void nn_block(const NNJob& J, int qbase, uint4* lds) {
-    uint4 qa[kNNPerThread][2];
-    int best[kNNPerThread];
-    const uint4* qg = reinterpret_cast<const uint4*>(J.q);
-#pragma unroll
-    for (int r = 0; r < kNNPerThread; ++r) {
-        int q = qbase + r * kNNThreads + threadIdx.x;
-        best[r] = 0x7FFFFFFF;
-        if (q < J.nq) {
-            qa[r][0] = qg[2 * q];
-            qa[r][1] = qg[2 * q + 1];
-        } else {
-            qa[r][0] = make_uint4(0, 0, 0, 0);
-            qa[r][1] = make_uint4(0, 0, 0, 0);
-        }
-    }
-    const uint4* tg = reinterpret_cast<const uint4*>(J.t);
-    for (int t0 = 0; t0 < J.nt; t0 += kTrainChunk) {
-        const int nc = min(kTrainChunk, J.nt - t0);
-        __syncthreads();
-        for (int i = threadIdx.x; i < nc * 2; i += kNNThreads) lds[i] = tg[2 * t0 + i];
-        __syncthreads();
-        for (int tt = 0; tt < nc; ++tt) {
-            const uint4 a = lds[2 * tt], b = lds[2 * tt + 1];
-            const int t = t0 + tt;
-#pragma unroll
-            for (int r = 0; r < kNNPerThread; ++r) {
-                int d = __popc(a.x ^ qa[r][0].x) + __popc(a.y ^ qa[r][0].y) + __popc(a.z ^ qa[r][0].z) +
-                        __popc(a.w ^ qa[r][0].w) + __popc(b.x ^ qa[r][1].x) + __popc(b.y ^ qa[r][1].y) +
-                        __popc(b.z ^ qa[r][1].z) + __popc(b.w ^ qa[r][1].w);
-                best[r] = min(best[r], (d << 16) | t);
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < kNNPerThread; ++r) {
-        int q = qbase + r * kNNThreads + threadIdx.x;
-        if (q < J.nq) J.out[q] = J.nt > 0 ? best[r] : -1;
-    }
-}
-
-__global__ __launch_bounds__(kNNThreads) void nn_stream_kernel(StreamParams P) {
-    extern __shared__ uint4 lds[];
-    const int p = blockIdx.z, dir = blockIdx.y;
-    const int fa = dir == 0 ? p : p + 1, fb = dir == 0 ? p + 1 : p;
-    NNJob J;
-    J.q = P.buf.desc + (int64_t)fa * P.plan.kp_cap * 32;
-    J.nq = min(P.buf.nkp[fa], P.plan.kp_cap);
-    J.t = P.buf.desc + (int64_t)fb * P.plan.kp_cap * 32;
-    J.nt = min(P.buf.nkp[fb], P.plan.kp_cap);
-    J.out = P.buf.nn + ((int64_t)dir * P.nframes + p) * P.plan.kp_cap;
-    const int qbase = blockIdx.x * kNNQ;
-    if (qbase >= J.nq) return;
-    nn_block(J, qbase, lds);
-}
-
-// Fused forward + backward nearest neighbours of one stream pair: every
-// distance is computed once.  A block owns 1024 queries of frame p (4 per
-// lane); the trains of frame p+1 stream through LDS.  Each wave takes 64
-// trains per pass (one per lane) and rotates them around the wave with DPP
-// wave_ror:1 for 64 rounds, so every lane meets every train; the row minimum
-// (forward NN) stays in the lane, the column minimum (backward NN) travels
-// with its train and is folded into LDS, then global, with atomicMin on packed
-// (distance << 16 | index) keys, which keeps OpenCV's first-index tie rule.
-constexpr int kFQ = 4, kFNT = 256, kFQB = kFQ * kFNT, kFChunk = 1024;
-
-__device__ __forceinline__ uint32_t ror1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);  // wave_ror:1
-}
-
-__global__ __launch_bounds__(kFNT) void nn_fused_kernel(StreamParams P) {
-    __shared__ uint4 lds[kFChunk * 2];
-    __shared__ int colmin[kFChunk];
-    const int p = blockIdx.y;
-    const int nq = min(P.buf.nkp[p], P.plan.kp_cap), nt = min(P.buf.nkp[p + 1], P.plan.kp_cap);
-    const int qbase = blockIdx.x * kFQB;
-    if (qbase >= nq) return;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint4* qg = reinterpret_cast<const uint4*>(P.buf.desc + (int64_t)p * P.plan.kp_cap * 32);
-    const uint4* tg = reinterpret_cast<const uint4*>(P.buf.desc + (int64_t)(p + 1) * P.plan.kp_cap * 32);
-    int32_t* fwd = P.buf.nn + (int64_t)p * P.plan.kp_cap;
-    int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * P.plan.kp_cap;
-    uint4 qa[kFQ][2];
-    int best[kFQ], qkey[kFQ];
-#pragma unroll
-    for (int r = 0; r < kFQ; ++r) {
-        const int q = qbase + (wid * kFQ + r) * 64 + lane;
-        best[r] = 0x7FFFFFFF;
-        qkey[r] = q < nq ? q : 0x7FFFFFFF;  // invalid queries never win a column
-        if (q < nq) {
-            qa[r][0] = qg[2 * q];
-            qa[r][1] = qg[2 * q + 1];
-        } else {
-            qa[r][0] = make_uint4(0, 0, 0, 0);
-            qa[r][1] = make_uint4(0, 0, 0, 0);
-        }
-    }
-    for (int t0 = 0; t0 < nt; t0 += kFChunk) {
-        const int nc = min(kFChunk, nt - t0);
-        __syncthreads();
-        for (int i = threadIdx.x; i < nc * 2; i += kFNT) lds[i] = tg[2 * t0 + i];
-        for (int i = threadIdx.x; i < nc; i += kFNT) colmin[i] = 0x7FFFFFFF;
-        __syncthreads();
-        for (int pass = 0; pass < nc; pass += 64) {
-            const int tt = pass + lane;
-            uint4 a, b;
-            if (tt < nc) {
-                a = lds[2 * tt];
-                b = lds[2 * tt + 1];
-            } else {
-                a = make_uint4(0, 0, 0, 0);
-                b = make_uint4(0, 0, 0, 0);
-            }
-            uint32_t tid = tt < nc ? (uint32_t)(t0 + tt) : 0xFFFFu;  // travels with the train
-            int cmin = 0x7FFFFFFF;
-            for (int r = 0; r < 64; ++r) {
-                const bool tv = tid != 0xFFFFu;
-#pragma unroll
-                for (int j = 0; j < kFQ; ++j) {
-                    const int d = __popc(a.x ^ qa[j][0].x) + __popc(a.y ^ qa[j][0].y) + __popc(a.z ^ qa[j][0].z) +
-                                  __popc(a.w ^ qa[j][0].w) + __popc(b.x ^ qa[j][1].x) + __popc(b.y ^ qa[j][1].y) +
-                                  __popc(b.z ^ qa[j][1].z) + __popc(b.w ^ qa[j][1].w);
-                    if (tv) best[j] = min(best[j], (d << 16) | (int)tid);
-                    cmin = min(cmin, qkey[j] == 0x7FFFFFFF ? 0x7FFFFFFF : (d << 16) | qkey[j]);
-                }
-                a.x = ror1(a.x);
-                a.y = ror1(a.y);
-                a.z = ror1(a.z);
-                a.w = ror1(a.w);
-                b.x = ror1(b.x);
-                b.y = ror1(b.y);
-                b.z = ror1(b.z);
-                b.w = ror1(b.w);
-                tid = ror1(tid);
-                cmin = (int)ror1((uint32_t)cmin);
-            }
-            // after 64 rotations every train is back in its home lane
-            if (tt < nc) atomicMin(&colmin[tt], cmin);
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < nc; i += kFNT)
-            if (colmin[i] != 0x7FFFFFFF) atomicMin(&bwd[t0 + i], colmin[i]);
-    }
-#pragma unroll
-    for (int r = 0; r < kFQ; ++r) {
-        const int q = qbase + (wid * kFQ + r) * 64 + lane;
-        if (q < nq) fwd[q] = nt > 0 ? best[r] : -1;
-    }
-}
 
 // Forward + backward nearest neighbours of one stream pair on the matrix cores.
 // Descriptor bits are +-1 bytes (desc_x, written by describe_kernel); scaled
@@ -248,11 +80,15 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
     }
 }
 
-__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs, int nqb) {
+// tsplit > 1 (the per-call path: one pair, so a short grid) gives each
+// workgroup a contiguous 1/tsplit of the train stages and folds the forward
+// keys with atomicMin too (fwd pre-filled with 0x7F7F7F7F).
+__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs, int nqb, int tsplit) {
     __shared__ v4i bt[2][kMStage * 16];
     __shared__ int colmin[2][kMStage];
     const int nwg = gridDim.x;  // a multiple of 8
-    const int L = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+    const int L0 = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+    const int L = L0 / tsplit, ts = L0 - L * tsplit;
     const int p = L / nqb, qb = L - p * nqb;
     if (p >= pairs) return;
     const int cap = P.plan.kp_cap;
@@ -279,7 +115,8 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
     // backward key base of register g: 2^20 + row(g); rows past nq never win (partial waves only)
     const int rowb = kKeyBase + qs + 4 * h;
     const bool full = qs + 64 <= nq;
-    const int nst = (nt + kMStage - 1) / kMStage;
+    const int nst_all = (nt + kMStage - 1) / kMStage;
+    const int st0 = (int)((int64_t)nst_all * ts / tsplit), nst = (int)((int64_t)nst_all * (ts + 1) / tsplit);
     v4i v[kMStage * 16 / 256];
     auto load_stage = [&](int st) {  // 4 chunks per thread (clamped index; zeroed past nt when stored)
 #pragma unroll
@@ -296,13 +133,13 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
         }
         if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;
     };
-    if (nst > 0) {
-        load_stage(0);
-        store_stage(0, 0);
+    if (st0 < nst) {
+        load_stage(st0);
+        store_stage(st0, 0);
     }
     __syncthreads();
-    for (int st = 0; st < nst; ++st) {
-        const int cur = st & 1;
+    for (int st = st0; st < nst; ++st) {
+        const int cur = (st - st0) & 1;
         if (st + 1 < nst) load_stage(st + 1);
         if (full) nn_stage<true>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
         else nn_stage<false>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
@@ -321,18 +158,41 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
 #pragma unroll
             for (int o = 1; o < 32; o <<= 1) vv = min(vv, __shfl_xor(vv, o));
             const int qr = qs + 32 * s2 + (g & 3) + 8 * (g >> 2) + 4 * h;
-            if (r == g && qr < nq) fwd[qr] = nt > 0 ? key_old(vv) : -1;
+            if (r == g && qr < nq) {
+                if (tsplit > 1) {
+                    if (st0 < nst) atomicMin(&fwd[qr], key_old(vv));
+                } else {
+                    fwd[qr] = nt > 0 ? key_old(vv) : -1;
+                }
+            }
         }
 }
 
-__global__ __launch_bounds__(kNNThreads) void nn_pair_kernel(const uint8_t* q, int nq, const uint8_t* t, int nt,
-                                                             int32_t* out) {
-    extern __shared__ uint4 lds[];
-    const int dir = blockIdx.y;
-    NNJob J{dir == 0 ? q : t, dir == 0 ? nq : nt, dir == 0 ? t : q, dir == 0 ? nt : nq, out + (dir == 0 ? 0 : nq)};
-    const int qbase = blockIdx.x * kNNQ;
-    if (qbase >= J.nq) return;
-    nn_block(J, qbase, lds);
+// Per-call operands: packed 32-byte descriptors (rows of q, then rows of t) to
+// the +-1 bytes nn_mfma_kernel reads (byte j of a row = bit j%8 of packed byte
+// j/8: any bijection works, both sides use the same), and the pair's counts.
+__global__ __launch_bounds__(256) void expand_desc_kernel(const uint8_t* __restrict__ q, int nq,
+                                                          const uint8_t* __restrict__ t, int nt, int cap,
+                                                          int8_t* __restrict__ x, int32_t* __restrict__ nkp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // (row, 16-byte chunk)
+    if (i == 0) {
+        nkp[0] = nq;
+        nkp[1] = nt;
+    }
+    const int row = i >> 4, c = i & 15;
+    if (row >= nq + nt) return;
+    const uint8_t* src = row < nq ? q + (int64_t)row * 32 : t + (int64_t)(row - nq) * 32;
+    const int slot = row < nq ? row : cap + (row - nq);
+    const uint32_t bits = (uint32_t)src[2 * c] | ((uint32_t)src[2 * c + 1] << 8);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v |= ((bits >> (4 * k + j)) & 1u ? 0x01u : 0xFFu) << (8 * j);
+        w[k] = v;
+    }
+    reinterpret_cast<uint4*>(x + (int64_t)slot * 256)[c] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 constexpr int kXNT = 1024;
@@ -438,12 +298,10 @@ __global__ __launch_bounds__(kXNT) void crosscheck_stream_kernel(StreamParams P,
 
 // Single pair (C-ABI dvo_bf_match_hamming): output in queryIdx order like
 // OpenCV (the caller's Python applies the stable distance sort itself).
-__global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* nn, int nq, int nt, int mode,
-                                                               dvo_dmatch* out, int* m_out) {
+__global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* fwd, const int32_t* bwd, int nq, int nt,
+                                                               int mode, dvo_dmatch* out, int* m_out) {
     __shared__ uint32_t keys[2 * kMaxSort];
     __shared__ int scan_lds[32];
-    const int32_t* fwd = nn;
-    const int32_t* bwd = nn + nq;
     const int m = crosscheck_sort(fwd, bwd, nq, nt, mode, keys, scan_lds);
     // re-sort by queryIdx: keys are unique (d<<16|q); rewrite as (q<<16|d) and sort again
     for (int i = threadIdx.x; i < m; i += kXNT) {
@@ -488,19 +346,48 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     if (e != hipSuccess) return e;
     const int pairs = P.nframes - 1, nqb = (cap + kMQB - 1) / kMQB;
     const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
-    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb);
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb, 1);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();
 }
 
-hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, int32_t* d_nn,
+namespace {
+int pair_cap(int nq, int nt) { return ((nq > nt ? nq : nt) + kMQB - 1) / kMQB * kMQB; }
+}  // namespace
+
+size_t match_pair_work_size(int nq, int nt) {
+    const size_t cap = (size_t)pair_cap(nq, nt);
+    return 256 + 2 * cap * 256 + 3 * cap * sizeof(int32_t);
+}
+
+// One pair through the stream's matcher: a StreamParams whose two "frames" are
+// the query and train sets (nkp = {nq, nt}, desc_x slots 0 and 1, nn = fwd |
+// unused | bwd), so nn_mfma_kernel runs unchanged, with the train stages split
+// over tsplit workgroups per query block to fill more than nq / 256 CUs.
+hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s) {
-    const int nmax = nq > nt ? nq : nt;
-    const size_t lds = (size_t)(nmax < kTrainChunk ? (nmax > 0 ? nmax : 1) : kTrainChunk) * 32;
-    dim3 grid((nmax + kNNQ - 1) / kNNQ, 2);
-    hipLaunchKernelGGL(nn_pair_kernel, grid, dim3(kNNThreads), lds, s, d_q, nq, d_t, nt, d_nn);
-    hipLaunchKernelGGL(crosscheck_pair_kernel, dim3(1), dim3(kXNT), 0, s, d_nn, nq, nt, cross_check, d_out, d_m);
+    const int cap = pair_cap(nq, nt);
+    StreamParams P{};
+    P.plan.kp_cap = cap;
+    P.nframes = 2;
+    uint8_t* w = static_cast<uint8_t*>(d_work);
+    P.buf.nkp = reinterpret_cast<int32_t*>(w);
+    P.buf.desc_x = reinterpret_cast<int8_t*>(w + 256);
+    P.buf.nn = reinterpret_cast<int32_t*>(w + 256 + 2 * (size_t)cap * 256);
+    int32_t* fwd = P.buf.nn;
+    int32_t* bwd = P.buf.nn + 2 * (size_t)cap;
+    hipError_t e = hipMemsetAsync(P.buf.nn, 0x7F, sizeof(int32_t) * 3 * (size_t)cap, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(expand_desc_kernel, dim3((unsigned)(((nq + nt) * 16 + 255) / 256)), dim3(256), 0, s, d_q, nq,
+                       d_t, nt, cap, P.buf.desc_x, P.buf.nkp);
+    const int nqb = cap / kMQB;
+    const int nst = (nt + kMStage - 1) / kMStage;
+    int tsplit = 1;
+    while (tsplit < 16 && nqb * tsplit * 2 <= 256 && nst >= tsplit * 4) tsplit *= 2;  // <= 256 workgroups, >= 2 stages each
+    const int nwg = ((nqb * tsplit + 7) / 8) * 8;
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, 1, nqb, tsplit);
+    hipLaunchKernelGGL(crosscheck_pair_kernel, dim3(1), dim3(kXNT), 0, s, fwd, bwd, nq, nt, cross_check, d_out, d_m);
     return hipGetLastError();
 }
 

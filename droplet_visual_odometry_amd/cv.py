@@ -21,6 +21,8 @@ on each.
 """
 from __future__ import annotations
 
+from collections.abc import Sequence
+
 import numpy as np
 
 from . import ops
@@ -81,23 +83,91 @@ class DMatch:
         return f"<DMatch q={self.queryIdx} t={self.trainIdx} d={self.distance}>"
 
 
-class KeyPointTuple(tuple):
-    """The tuple of KeyPoint objects detectAndCompute returns, carrying the raw
-    structured array (KEYPOINT_DTYPE) so KeyPoint_convert needs no Python loop."""
-    array: np.ndarray
+class KeyPoints(Sequence):
+    """The keypoint sequence detectAndCompute returns (cv2 returns a tuple of
+    KeyPoint), backed by the structured array the library wrote
+    (KEYPOINT_DTYPE).  KeyPoint objects are built on first access, so a frame's
+    2000 keypoints cost no Python objects until someone indexes them;
+    KeyPoint_convert and the drop-in's match gather work on the array."""
+    __slots__ = ("array", "_objs")
+
+    def __init__(self, array: np.ndarray):
+        self.array = array
+        self._objs = None
+
+    def __len__(self):
+        return len(self.array)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return KeyPoints(self.array[i])
+        n = len(self.array)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("keypoint index out of range")
+        if self._objs is None:
+            self._objs = [None] * n
+        k = self._objs[i]
+        if k is None:
+            k = self._objs[i] = KeyPoint(*self.array[i].tolist())
+        return k
+
+    def take(self, idx) -> "KeyPoints":
+        """Keypoints at the given indices (a gather on the array)."""
+        return KeyPoints(self.array[np.asarray(idx, np.int64)])
+
+    def __add__(self, other):
+        return tuple(self) + tuple(other)
+
+    def __repr__(self):
+        return f"<KeyPoints n={len(self)}>"
 
 
-def _keypoints_from_array(arr: np.ndarray) -> KeyPointTuple:
-    rows = arr.tolist()
-    t = KeyPointTuple(KeyPoint(*r) for r in rows)
-    t.array = arr
-    return t
+class DMatches(Sequence):
+    """The match sequence BFMatcher.match returns, backed by a DMATCH_DTYPE
+    array; DMatch objects are built on first access."""
+    __slots__ = ("array", "_objs")
+
+    def __init__(self, array: np.ndarray):
+        self.array = array
+        self._objs = None
+
+    def __len__(self):
+        return len(self.array)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return DMatches(self.array[i])
+        n = len(self.array)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError("match index out of range")
+        if self._objs is None:
+            self._objs = [None] * n
+        m = self._objs[i]
+        if m is None:
+            r = self.array[i]
+            m = self._objs[i] = DMatch(int(r["queryIdx"]), int(r["trainIdx"]), int(r["imgIdx"]), float(r["distance"]))
+        return m
+
+    def sorted_by_distance(self) -> "DMatches":
+        """sorted(matches, key=lambda m: m.distance) (visual_odometry_v3.py:221):
+        Python's sort is stable, so is this argsort."""
+        return DMatches(self.array[np.argsort(self.array["distance"], kind="stable")])
+
+    def __add__(self, other):
+        return list(self) + list(other)
+
+    def __repr__(self):
+        return f"<DMatches n={len(self)}>"
 
 
 def KeyPoint_convert(keypoints, keypointIndexes=None):
     """float32[N, 2] of keypoint coordinates (cv2.KeyPoint_convert)."""
-    arr = getattr(keypoints, "array", None)
-    if arr is not None and keypointIndexes is None:
+    if isinstance(keypoints, KeyPoints):
+        arr = keypoints.array if keypointIndexes is None else keypoints.array[np.asarray(keypointIndexes, np.int64)]
         return np.stack([arr["x"], arr["y"]], axis=1).astype(np.float32)
     kps = keypoints if keypointIndexes is None else [keypoints[i] for i in keypointIndexes]
     if len(kps) == 0:
@@ -132,7 +202,7 @@ class ORB:
             kps, desc = ops.detect_and_compute(img, self.nfeatures, self.fastThreshold)
         except DVOError as e:
             raise error(str(e)) from e
-        return _keypoints_from_array(kps), (desc if len(kps) else None)
+        return KeyPoints(kps), (desc if len(kps) else None)
 
     def detect(self, image, mask=None):
         return self.detectAndCompute(image, mask)[0]
@@ -211,7 +281,7 @@ class BFMatcher:
             m = ops.bf_match(q, t, mode)
         except DVOError as e:
             raise error(str(e)) from e
-        return [DMatch(int(a), int(b), 0, float(d)) for a, b, d in zip(m["queryIdx"], m["trainIdx"], m["distance"])]
+        return DMatches(m)
 
     def knnMatch(self, queryDescriptors, trainDescriptors, k, mask=None, compactResult=False):
         """List (one per query) of up to k DMatch in ascending distance."""
@@ -394,7 +464,7 @@ def drawKeypoints(image, keypoints, outImage=None, color=(0, 255, 0), flags=0):
     The reference computes and discards this image (v3:375, D6)."""
     img = np.asarray(image)
     out = np.repeat(img[..., None], 3, axis=2).copy() if img.ndim == 2 else img.copy()
-    arr = getattr(keypoints, "array", None)
+    arr = keypoints.array if isinstance(keypoints, KeyPoints) else None
     if arr is not None:
         xs = np.rint(arr["x"]).astype(np.int64)
         ys = np.rint(arr["y"]).astype(np.int64)

@@ -37,6 +37,35 @@ def build(force: bool = False) -> str:
     return _LIB_PATH
 
 
+def host_cpu():
+    """(model name, tag): the host CPU's model and a hash of its model + flags."""
+    import hashlib
+    model, flags = "unknown", ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and model == "unknown":
+                model = line.split(":", 1)[1].strip()
+            elif line.startswith("flags") and not flags:
+                flags = line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return model, hashlib.sha1((model + "|" + flags).encode()).hexdigest()[:10]
+
+
+def use_native_build() -> str:
+    """Switch this module to the -O3 -march=native build of the same sources
+    (the CPU baseline; built here for this host CPU on first use).  Results
+    are identical to the default build (no contraction, no fast-math)."""
+    global _lib, _LIB_PATH
+    tag = host_cpu()[1]
+    path = os.path.join(_HERE, "build", f"libdvo_oracle_native_{tag}.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "native", f"NATIVE_TAG={tag}"])
+    if _LIB_PATH != path:
+        _LIB_PATH, _lib = path, None
+    return path
+
+
 def lib():
     global _lib
     if _lib is None:

@@ -60,3 +60,39 @@ def test_visual_odometry_replay(gpu_ctx, oracle_mod, tmp_path):
         np.testing.assert_allclose(rel, T_rel, rtol=0, atol=1e-12)
         np.testing.assert_allclose(T_vo, T_ref, rtol=0, atol=1e-12)
     assert len(vo.frame_translations) == 4 and len(vo.projection_matrix_list) == 4
+
+
+def test_array_backed_matches_equal_object_path(gpu_ctx, frames_640):
+    """The drop-in's ORB branch on cv.DMatches / cv.KeyPoints (stable argsort +
+    index gather) returns what the reference's object loop returns
+    (sorted(matches, key=distance), then prev_kp[m.queryIdx], cur_kp[m.trainIdx],
+    v3:219-238) on plain lists of the same objects."""
+    from droplet_visual_odometry_amd import cv
+    sys.path.insert(0, os.path.join(ROOT, "droplet_visual_odometry_amd", "dropin"))
+    try:
+        import visual_odometry_v3 as v3
+    finally:
+        sys.path.pop(0)
+    frames, _ = frames_640
+    orb = cv.ORB_create(nfeatures=1000)
+    kp0, d0 = orb.detectAndCompute(frames[0], None)
+    kp1, d1 = orb.detectAndCompute(frames[1], None)
+    assert isinstance(kp0, cv.KeyPoints) and len(kp0) == len(d0)
+    bf = cv.BFMatcher(normType=cv.NORM_HAMMING, crossCheck=True)
+    me = types.SimpleNamespace(mode="orb", bf=bf)
+    matches, top_prev, top_cur = v3.VisualOdometry.get_matches_between_two_frames(me, kp0, d0, kp1, d1)
+    ref = sorted(list(bf.match(d0, d1)), key=lambda x: x.distance)
+    assert [(m.queryIdx, m.trainIdx, m.distance) for m in matches] == \
+        [(m.queryIdx, m.trainIdx, m.distance) for m in ref]
+    assert [k.pt for k in top_prev] == [kp0[m.queryIdx].pt for m in ref]
+    assert [k.pt for k in top_cur] == [kp1[m.trainIdx].pt for m in ref]
+    # lists of plain KeyPoint objects take the reference's loop and agree
+    _, lp, lc = v3.VisualOdometry.get_matches_between_two_frames(me, list(kp0), d0, list(kp1), d1)
+    np.testing.assert_array_equal(cv.KeyPoint_convert(lp), cv.KeyPoint_convert(top_prev))
+    np.testing.assert_array_equal(cv.KeyPoint_convert(lc), cv.KeyPoint_convert(top_cur))
+    # the lazily drawn keypoint image (v3:375) is the eager one
+    vo = types.SimpleNamespace(feature_detector=orb, _features=v3._FeatureCache())
+    kps, desc, drawn = v3.VisualOdometry.compute_current_image_elements(vo, frames[2])
+    np.testing.assert_array_equal(np.asarray(drawn),
+                                  cv.drawKeypoints(frames[2], kps, None, color=(0, 255, 0), flags=0))
+    assert drawn.shape == (480, 640, 3)

@@ -127,3 +127,26 @@ def test_stream_end_to_end_640(gpu_ctx, oracle_mod, frames_640):
         np.testing.assert_array_equal(r["R"].reshape(3, 3), ref["R"])
         np.testing.assert_array_equal(r["t"], ref["t_unit"].ravel())
         assert r["n_good"] == ref["good"]
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 1), (5, 300), (63, 64), (257, 255), (2000, 2000), (4000, 3500), (700, 8192),
+                                   (8192, 8192)])
+def test_bf_match_sizes(gpu_ctx, oracle_mod, nq, nt):
+    """Per-call BFMatcher(NORM_HAMMING).match (v3:219) on the MFMA matcher at
+    ragged sizes up to the 8192 cap, every crossCheck mode, bit-exact.  Half the
+    descriptors are low-entropy (few set bits), so distance ties across the
+    train split and the LDS stages are common."""
+    from droplet_visual_odometry_amd import ops
+    rng = np.random.default_rng(nq * 7 + nt)
+    dq = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    dt = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    dq[::2] &= rng.integers(0, 256, (len(dq[::2]), 32), dtype=np.uint8) & 0x11
+    dt[::2] &= rng.integers(0, 256, (len(dt[::2]), 32), dtype=np.uint8) & 0x11
+    if nt > 4:
+        dt[nt // 2] = dt[1]  # an exact duplicate train: the lower index must win
+    for mode in (0, 1, 2):
+        q, t, d = oracle_mod.bf_match(dq, dt, mode)
+        got = ops.bf_match(dq, dt, mode, ctx=gpu_ctx)
+        np.testing.assert_array_equal(got["queryIdx"], q)
+        np.testing.assert_array_equal(got["trainIdx"], t)
+        np.testing.assert_array_equal(got["distance"], d)
