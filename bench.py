@@ -36,7 +36,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-PMC_TRAFFIC = "r01i_pmc_traffic.json"  # tools/profile_round.sh: FETCH_SIZE / WRITE_SIZE passes of the current kernels
+# VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
+VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
+PMC_TRAFFIC = "r02_pmc_traffic.json"  # tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes of the kernels
 
 
 def parse():
@@ -178,9 +180,21 @@ def main():
         dom = max(single, key=lambda k: per_call.get(k, 0.0))
         bytes_per_launch = sb[dom] * (B + 1)
         achieved = bytes_per_launch / (per_call[dom] * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(single[dom], W, H, N, B)
+        pmc = pmc_counts(single[dom], W, H, N, B)
+        valu = None
+        if pmc and pmc["valu_insts"]:
+            va = pmc["valu_insts"] / (per_call[dom] * 1e-3)
+            valu = {"achieved": round(va / 1e9, 3), "peak": VALU_PEAK_WIPS / 1e9, "unit": "G wave-instructions/s",
+                    "frac": round(va / VALU_PEAK_WIPS, 6), "insts_per_launch": round(pmc["valu_insts"]),
+                    "note": "SQ_INSTS_VALU per launch / the launch's HIP-event time; peak = one wave64 VALU "
+                            "instruction per 2 cycles per SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)"}
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic, "traffic_source": traffic_src,
+                    "frac": round(achieved / HBM_PEAK_GBS, 6),
+                    "traffic": pmc["traffic"] if pmc else None,
+                    "traffic_raw": pmc["traffic_raw"] if pmc else None,
+                    "traffic_calibrated": pmc["calibrated"] if pmc else None,
+                    "traffic_source": pmc["source"] if pmc else None,
+                    "valu": valu, "valu_frac": valu["frac"] if valu else None,
                     "kernel": single[dom], "algorithmic_bytes_per_launch": bytes_per_launch,
                     "kernel_ms_per_launch": round(per_call[dom], 4),
                     "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
@@ -377,24 +391,28 @@ def chained_ate(fs, pool, corners, K, ref, B):
     return float(np.sqrt(np.mean(err))) if err else None
 
 
-def pmc_traffic(kernel, W, H, N, B):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/PMC_TRAFFIC: FETCH_SIZE + WRITE_SIZE), when they were
-    taken on this configuration; PMC counters cannot run inside the timed loop."""
+def pmc_counts(kernel, W, H, N, B):
+    """Per-launch PMC figures of `kernel` from the committed round profile
+    (profiles/PMC_TRAFFIC, tools/profile_round.sh): HBM bytes (FETCH_SIZE +
+    WRITE_SIZE, corrected by the known-bytes calibration of the kernel's access
+    widths) and SQ_INSTS_VALU, scaled per frame from the profiled batch to a
+    launch over B + 1 frames.  PMC counters cannot run inside the timed loop."""
     path = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
     try:
         doc = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
+        return None
     c = doc.get("config", {})
     k = doc.get("kernels", {}).get(kernel)
     if k is None or (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
-        return None, None
-    # one launch covers B + 1 frames: the counted bytes scale per frame from the profiled batch
+        return None
     scale = (B + 1) / (c["batch"] + 1)
-    src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE at batch {c['batch']}"
+    src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc passes at batch {c['batch']}"
     src += ")" if c["batch"] == B else f", scaled per frame to batch {B})"
-    return round((k["fetch_bytes"] + k["write_bytes"]) * scale), src
+    return {"traffic": round((k["fetch_bytes"] + k["write_bytes"]) * scale),
+            "traffic_raw": round((k["fetch_bytes_raw"] + k["write_bytes_raw"]) * scale),
+            "calibrated": bool(k.get("calibrated")), "widths": k.get("widths"),
+            "valu_insts": k.get("SQ_INSTS_VALU", 0.0) * scale, "source": src}
 
 
 def dropin_rate(pool, corners, K, nfeatures, seconds, n_frames=48):

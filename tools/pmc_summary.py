@@ -1,4 +1,4 @@
-"""Aggregate a rocprofv3 --pmc counter_collection.csv per kernel (dvo:: only).
+"""Aggregate a rocprofv3 --pmc counter_collection.csv per kernel (dvo:: and the calib_ kernels).
 
 usage: python tools/pmc_summary.py <counter_collection.csv> [out.csv]
 Prints, per kernel, the mean over dispatches of every collected counter."""
@@ -12,7 +12,7 @@ def main(src, dst=None):
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(src)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
-        if "dvo::" not in name:
+        if "dvo::" not in name and not name.startswith("calib_"):
             continue
         k = name.replace("(anonymous namespace)::", "").split("(")[0].replace("dvo::", "")
         did = r.get("Dispatch_Id") or r.get("Dispatch-Id")

@@ -1,28 +1,59 @@
-"""Merge the FETCH_SIZE and WRITE_SIZE pass summaries (tools/pmc_summary.py
-output) into the per-launch HBM traffic file bench.py reads for roofline.traffic.
+"""Merge the PMC passes of a round profile into the per-launch file bench.py
+reads for roofline.traffic and roofline.valu.
 
-usage: python tools/pmc_traffic.py <fetch.csv> <write.csv> <out.json> [batch]
-rocprofv3 reports both counters in KB; x1024 is applied. The default bench
-configuration (1280x720, 2000 features, the given batch (default 1024), one
-stream) is recorded."""
+usage: python tools/pmc_traffic.py <fetch.csv> <write.csv> <sq.csv> <calibration.json> <out.json> [batch]
+
+fetch/write: FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py output;
+rocprofv3 reports KB, x1024 applied).  sq: the SQ_INSTS_* pass.  calibration:
+tools/pmc_calibrate.py output; a kernel's readings are multiplied by the
+factor of the access width it uses (KERNEL_WIDTHS, from the kernel source);
+kernels not listed keep their raw readings (calibrated: false)."""
 import csv
 import json
 import sys
 
+# (read width, write width) of the dominant accesses, per kernel (orb.hip)
+KERNEL_WIDTHS = {
+    "fast_strip_kernel": ("b32_buffer", "b32_global"),  # raw_buffer_load_b32 rows; 4-byte key / count stores
+    "blur_kernel": ("b32_buffer", "b32_global"),        # raw_buffer_load_b32 rows; one word per lane and row
+}
 
-def load(path, counter):
-    return {r["kernel"]: float(r[counter]) * 1024.0 for r in csv.DictReader(open(path)) if counter in r}
+
+def load(path, counters):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        out[r["kernel"]] = {c: float(r[c]) for c in counters if c in r and r[c] != ""}
+    return out
 
 
-def main(fetch, write, dst, batch=1024):
-    f, w = load(fetch, "FETCH_SIZE"), load(write, "WRITE_SIZE")
+def main(fetch, write, sq, calib, dst, batch=1024):
+    f = load(fetch, ["FETCH_SIZE"])
+    w = load(write, ["WRITE_SIZE"])
+    s = load(sq, ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
+                  "SQ_INSTS_VMEM_WR", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"])
+    cal = json.load(open(calib))
+    kernels = {}
+    for k in sorted(set(f) | set(w) | set(s)):
+        fr = f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024.0
+        wr = w.get(k, {}).get("WRITE_SIZE", 0.0) * 1024.0
+        e = {"fetch_bytes_raw": fr, "write_bytes_raw": wr}
+        if k in KERNEL_WIDTHS:
+            rw, ww = KERNEL_WIDTHS[k]
+            fa, wa = cal["read"][rw]["factor"], cal["write"][ww]["factor"]
+            e.update(fetch_bytes=fr * fa, write_bytes=wr * wa, calibrated=True,
+                     widths={"read": rw, "write": ww, "read_factor": fa, "write_factor": wa})
+        else:
+            e.update(fetch_bytes=fr, write_bytes=wr, calibrated=False)
+        for c, v in s.get(k, {}).items():
+            e[c] = v
+        kernels[k] = e
     doc = {
         "config": {"width": 1280, "height": 720, "nfeatures": 2000, "batch": int(batch), "streams": 1},
-        "unit": "bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE are KB; x1024 applied)",
-        "note": "separate --pmc passes (FETCH_SIZE, WRITE_SIZE), mean over dispatches; the byte kernels "
-                "load 4-16 B/lane, for which the guide's x2 FETCH_SIZE correction (16 B/lane streaming reads) "
-                "is not calibrated, so the raw value is reported",
-        "kernels": {k: {"fetch_bytes": f.get(k, 0.0), "write_bytes": w.get(k, 0.0)} for k in sorted(set(f) | set(w))},
+        "unit": "per launch: bytes (FETCH_SIZE/WRITE_SIZE KB x1024, then the width calibration), "
+                "SQ_* instruction counts (wave-level)",
+        "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts), mean over dispatches",
+        "calibration": calib,
+        "kernels": kernels,
     }
     json.dump(doc, open(dst, "w"), indent=1)
 

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round profile of the default bench command: rocprofv3 --kernel-trace --stats,
-# then one FETCH_SIZE and one WRITE_SIZE --pmc pass (separate runs, short bench),
-# merged into gpurun_out/prof/<tag>_pmc_traffic.json.   usage: tools/profile_round.sh TAG
+# then separate --pmc passes over a short bench (FETCH_SIZE; WRITE_SIZE; SQ
+# instruction counts) and over the known-bytes calibration kernels
+# (tools/calib, FETCH_SIZE; WRITE_SIZE), merged into
+# gpurun_out/prof/<tag>_pmc_traffic.json.   usage: tools/profile_round.sh TAG [bench args]
 set -e
 tag=$1; shift
 root=$(pwd)
@@ -9,12 +11,19 @@ out="$root/gpurun_out/prof"
 mkdir -p "$out"
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/st_$tag -o run --output-format csv -- python3 "$root/bench.py" "$@" > "$out/${tag}_bench_under_rocprof.log" 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/st_$tag -o run --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --dropin-seconds 0 "$@" > "$out/${tag}_bench_under_rocprof.log" 2>&1
 python3 "$root/tools/summarize_profile.py" $(find /tmp/st_$tag -name '*kernel_stats.csv') "$out/${tag}_kernel_stats.csv" > "$out/${tag}_kernel_stats.txt"
+short="--steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --dropin-seconds 0 --no-profile --batch 512"
 for c in FETCH_SIZE WRITE_SIZE; do
   # batch 512: the counter passes serialise every dispatch; traffic per frame is what bench.py scales
-  timeout -s KILL 170 rocprofv3 --pmc $c -d /tmp/pmc_${tag}_$c -o run --output-format csv -- python3 "$root/bench.py" --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --no-profile --batch 512 > "$out/${tag}_pmc_$c.log" 2>&1
+  timeout -s KILL 170 rocprofv3 --pmc $c -d /tmp/pmc_${tag}_$c -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_$c.log" 2>&1
   python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_$c -name '*counter_collection.csv') "$out/${tag}_pmc_$c.csv" > /dev/null
+  timeout -s KILL 60 rocprofv3 --pmc $c -d /tmp/cal_${tag}_$c -o run --output-format csv -- "$root/tools/calib/build/pmc_calib" > "$out/${tag}_calib_known.jsonl" 2> "$out/${tag}_calib_$c.log"
+  python3 "$root/tools/pmc_summary.py" $(find /tmp/cal_${tag}_$c -name '*counter_collection.csv') "$out/${tag}_calib_$c.csv" > /dev/null
 done
-python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_traffic.json" 512
-rm -rf /tmp/st_$tag /tmp/pmc_${tag}_*
+timeout -s KILL 170 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+  -d /tmp/pmc_${tag}_sq -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_sq.log" 2>&1
+python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_sq -name '*counter_collection.csv') "$out/${tag}_pmc_sq.csv" > /dev/null
+python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" > /dev/null
+python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512
+rm -rf /tmp/st_$tag /tmp/pmc_${tag}_* /tmp/cal_${tag}_*
