@@ -20,7 +20,8 @@ except Exception:  # pragma: no cover - torch is always present in this image
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # DVO_LIB_PATH: an experiment build of the same sources (tools/ A/B runs); default the in-tree product build
-LIB_PATH = os.environ.get("DVO_LIB_PATH") or os.path.join(HERE, "lib", "libdvo_hip.so")
+_DEFAULT_LIB = os.path.join(HERE, "lib", "libdvo_hip.so")
+LIB_PATH = os.environ.get("DVO_LIB_PATH") or _DEFAULT_LIB
 
 DVO_OK = 0
 DVO_EINVAL = -1
@@ -76,6 +77,7 @@ _i64 = ctypes.c_int64
 
 _SIGNATURES = {
     "dvo_version": ([], _c),
+    "dvo_build_id": ([], ctypes.c_char_p),
     "dvo_ctx_create": ([ctypes.POINTER(_vp), _c], _c),
     "dvo_ctx_destroy": ([_vp], None),
     "dvo_last_error": ([_vp], ctypes.c_char_p),
@@ -129,6 +131,12 @@ def load_library(path: str = LIB_PATH):
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        if path == _DEFAULT_LIB and os.path.isdir(os.path.join(HERE, "csrc")):
+            from .build import source_hash
+            want, got = source_hash(), L.dvo_build_id().decode()
+            if got != want:
+                raise ImportError(f"{path} was built from other sources (build id {got}, sources {want}): "
+                                  "rebuild it with `python -m droplet_visual_odometry_amd.build`")
         _lib = L
         return L
 

@@ -51,14 +51,40 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _stale(objs, lib=LIB):
-    if not os.path.exists(lib):
-        return True
-    t = os.path.getmtime(lib)
-    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
-        os.path.join(HERE, "..", "include", "dvo.h"), os.path.join(HERE, "..", "data", "orb_bit_pattern_31.inc"),
-        __file__]
-    return any(os.path.getmtime(d) > t for d in deps)
+def inputs():
+    """Every file the library is compiled from."""
+    return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [
+        os.path.normpath(os.path.join(HERE, "..", "include", "dvo.h")),
+        os.path.normpath(os.path.join(HERE, "..", "data", "orb_bit_pattern_31.inc"))]
+
+
+def source_hash(defines=()) -> str:
+    """Build id: sha256 over the source texts, the compiler flags and the
+    defines (16 hex digits).  Compiled into the library (dvo_build_id) and
+    checked when it is loaded, so a library built from other sources is
+    rebuilt here and refused on the GPU box, whatever the file times say."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in inputs():
+        h.update(os.path.relpath(path, os.path.dirname(HERE)).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read() + b"\0")
+    h.update(repr((CXXFLAGS, sorted(FILE_FLAGS.items()), ARCH, list(defines))).encode())
+    return h.hexdigest()[:16]
+
+
+def library_build_id(lib=LIB):
+    """dvo_build_id() of a built library, read from its bytes (no load)."""
+    try:
+        data = open(lib, "rb").read()
+    except OSError:
+        return None
+    i = data.find(b"DVO_BUILD_ID=")
+    return data[i + 13:i + 29].decode() if i >= 0 else None
+
+
+def _stale(lib, want):
+    return library_build_id(lib) != want
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()) -> str:
@@ -71,14 +97,16 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     os.makedirs(objdir, exist_ok=True)
     srcs = sources()
     objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
-    if not force and not _stale(objs, LIB):
+    bid = source_hash(defines)
+    if not force and not _stale(LIB, bid):
         return LIB
 
     def compile_one(pair):
         src, obj = pair
         lang = ["-x", "hip"]
         extra = [t for d in defines for t in (d.split() if d.startswith("-") else [f"-D{d}"])]  # raw flags pass through
-        cmd = [hipcc, *lang, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
+        cmd = [hipcc, *lang, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra,
+               f'-DDVO_BUILD_ID="{bid}"', "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -387,6 +387,13 @@ extern "C" {
 
 int dvo_version(void) { return 1; }
 
+#ifndef DVO_BUILD_ID
+#define DVO_BUILD_ID "unstamped0000000"
+#endif
+// "DVO_BUILD_ID=" + 16 hex digits: build.py finds it in the file without loading it
+static const char kBuildTag[] = "DVO_BUILD_ID=" DVO_BUILD_ID;
+const char* dvo_build_id(void) { return kBuildTag + 13; }
+
 int dvo_ctx_create(dvo_ctx** out, int device) {
     if (!out) return DVO_EINVAL;
     *out = nullptr;

@@ -26,25 +26,6 @@
 
 namespace dvo {
 
-#ifdef DVO_PROBE
-// Development probe (tools/probe_ransac.py): shader-clock cycles per phase,
-// accumulated by lane 0 of block 0 only.
-__device__ unsigned long long g_probe[32];
-#define PROBE_DECL unsigned long long _pt = __builtin_amdgcn_s_memtime()
-#define PROBE_MARK(i)                                                                 \
-    do {                                                                              \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
-            unsigned long long _n = __builtin_amdgcn_s_memtime();                      \
-            atomicAdd(&g_probe[i], _n - _pt);                                         \
-            _pt = _n;                                                                 \
-        } else {                                                                      \
-            _pt = __builtin_amdgcn_s_memtime();                                       \
-        }                                                                             \
-    } while (0)
-#else
-#define PROBE_DECL
-#define PROBE_MARK(i)
-#endif
 
 struct Cx {
     double re, im;
@@ -737,7 +718,6 @@ constexpr int kRecDoubles = 128;
 // overwritten in place by the solution rows 4..9).
 __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, double* Gg, double* R) {
     double* const G = Gg + 100 * 64;
-    PROBE_DECL;
     double At[9][9], W[5], Vt[5][5];
 #pragma unroll
     for (int i = 0; i < 9; ++i)
@@ -756,9 +736,7 @@ __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, 
         At[i][7] = y1 + 0.0;
         At[i][8] = 1.0;
     }
-    PROBE_MARK(10);
     jacobi_svd<9, 5, 9, 9>(At, W, Vt);
-    PROBE_MARK(11);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -777,14 +755,12 @@ __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, 
         for (int r = 0; r < 10; ++r)
 #pragma unroll
             for (int k = 0; k < 10; ++k) L[r][k] = Gg[(r * 10 + k) * 64];
-        PROBE_MARK(12);
         if (lu10_factor(L, piv)) {
             lu10_solve_cols(L, piv, G, G);
         } else {
 #pragma unroll
             for (int k = 40; k < 100; ++k) G[k * 64] = 0;
         }
-        PROBE_MARK(13);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const double* a1 = G + (i * 2 + 4) * 10 * 64;
@@ -844,14 +820,12 @@ __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, 
         c10 = ck;
     }
     R[kRecGeneric * 64] = fabs(c10) > DBL_EPSILON ? 0.0 : 1.0;
-    PROBE_MARK(14);
 }
 
 // Stage C: roots -> (x, y, z) by the 3x3 null space of B(z) -> E, normalised.
 // Polynomials flagged generic (leading coefficient negligible) are solved here.
 __device__ __forceinline__ void dk_store(double* R, Cx (&roots)[10]);
 __device__ __forceinline__ int fp_stage_c(double* R, double* models) {
-    PROBE_DECL;
     if (R[kRecGeneric * 64] == 2.0) {
         double c[11];
         Cx roots[10];
@@ -910,7 +884,6 @@ __device__ __forceinline__ int fp_stage_c(double* R, double* models) {
         for (int k = 0; k < 9; ++k) out[k] = e[k] * inv_n + 0.0;
         count++;
     }
-    PROBE_MARK(16);
     return count;
 }
 
@@ -1833,15 +1806,3 @@ hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n,
 }
 
 }  // namespace dvo
-
-#ifdef DVO_PROBE
-extern "C" int dvo_debug_probe(unsigned long long* out, int n, int reset) {
-    if (n > 32) n = 32;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dvo::g_probe), n * sizeof(unsigned long long)) != hipSuccess) return -4;
-    if (reset) {
-        unsigned long long z[32] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(dvo::g_probe), z, sizeof(z)) != hipSuccess) return -4;
-    }
-    return 0;
-}
-#endif

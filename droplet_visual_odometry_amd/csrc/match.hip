@@ -573,6 +573,10 @@ __global__ __launch_bounds__(256) void knn_pack_u8_kernel(const float* __restric
 #define DVO_KNN_U8Q 2
 #endif
 constexpr int kKnnU8Q = DVO_KNN_U8Q;  // queries per thread in knn_u8_kernel
+#ifndef DVO_KNN_RANGE_QB
+#define DVO_KNN_RANGE_QB (256 * DVO_KNN_U8Q)
+#endif
+constexpr int kKnnRangeQB = DVO_KNN_RANGE_QB;  // queries per workgroup the train split is sized for
 
 template <int D, int NORM, int K>
 __global__ __launch_bounds__(256) void knn_u8_kernel(const uint32_t* __restrict__ q, const uint32_t* __restrict__ qn,
@@ -777,16 +781,11 @@ hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int n
 }  // namespace
 
 int knn_ranges(int nq, int nt, int cus) {
-    // about one round of resident workgroups, at least 16 trains per range
-    const int qblocks = (nq + kKnnQ - 1) / kKnnQ;
-#ifndef DVO_KNN_ROUNDS
-#define DVO_KNN_ROUNDS 2
-#endif
-#ifdef DVO_KNN_FIXED
-    int ranges = (nt + kKnnTC - 1) / kKnnTC;
-#else
-    int ranges = (cus * kKnnWgPerCu * DVO_KNN_ROUNDS) / qblocks;
-#endif
+    // about two rounds of resident workgroups of the byte kernel (knn_u8_kernel,
+    // the path every SIFT call takes: kKnnRangeQB queries per workgroup), at
+    // least 16 trains per range; the float kernel shares the split
+    const int qblocks = (nq + kKnnRangeQB - 1) / kKnnRangeQB;
+    int ranges = (cus * kKnnWgPerCu * 2) / qblocks;
     ranges = std::min(ranges, (nt + 15) / 16);
     ranges = std::max(ranges, 1);
     const int range = (nt + ranges - 1) / ranges;

@@ -1333,7 +1333,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
             hipLaunchKernelGGL(resize_level_lds_kernel,
                                dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR), F), dim3(256), 0,
                                s, P, l);
-        else
+        else  // level pairs whose rounded sizes differ by more than 1.25x: tiny frames (8x8: levels 4->5, 6->7)
             hipLaunchKernelGGL(resize_level_kernel, dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsR - 1) / (4 * kRsR), F),
                                dim3(256), 0, s, P, l);
     }

@@ -59,6 +59,8 @@ typedef struct {
 } dvo_orb_params;
 
 int dvo_version(void);
+/* Source hash the library was built from (16 hex digits; build.py source_hash). */
+const char* dvo_build_id(void);
 int dvo_ctx_create(dvo_ctx** out, int device);
 void dvo_ctx_destroy(dvo_ctx* ctx);
 const char* dvo_last_error(const dvo_ctx* ctx);

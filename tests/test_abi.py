@@ -81,3 +81,12 @@ def test_record_layout_matches_header():
     assert PAIR_RECORD_DTYPE.itemsize == 256
     src = open(os.path.join(ROOT, "include", "dvo.h")).read()
     assert "256" in src
+
+
+def test_library_build_id_is_the_source_hash(libpath):
+    """The library carries the hash of the sources it was built from; loading
+    checks it, so a stale prebuilt library is refused rather than used."""
+    from droplet_visual_odometry_amd import _native, build
+    lib = _native.load_library()
+    assert lib.dvo_build_id().decode() == build.source_hash() == build.library_build_id(libpath)
+    assert build.source_hash(defines=("DVO_BLUR_TH=64",)) != build.source_hash()
