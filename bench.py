@@ -249,7 +249,8 @@ def main():
                    "parallelism": "single GPU",
                    "streams_in_flight": S,
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
-                   "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0},
+                   "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0,
+                   "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "pose_check": pose_check,

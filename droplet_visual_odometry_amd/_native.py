@@ -40,7 +40,8 @@ DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<
 PAIR_RECORD_DTYPE = np.dtype([("R", "<f8", (9,)), ("t", "<f8", (3,)), ("E", "<f8", (9,)),
                               ("n_kp_prev", "<i4"), ("n_kp_cur", "<i4"), ("n_matches", "<i4"),
                               ("n_inliers", "<i4"), ("n_good", "<i4"), ("ransac_iters", "<i4"),
-                              ("status", "<i4"), ("n_models", "<i4"), ("reserved", "<f8", (7,))])
+                              ("status", "<i4"), ("n_models", "<i4"), ("n_hypotheses", "<i4"), ("pad0", "<i4"),
+                              ("reserved", "<f8", (6,))])
 assert PAIR_RECORD_DTYPE.itemsize == 256
 
 

@@ -1537,7 +1537,9 @@ __global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec)
                : (P.buf.nkp[p] == 0 || P.buf.nkp[p + 1] == 0) ? DVO_ENOFEAT
                                                               : info[3];
     r.n_models = info[0] / 3;
-    for (int k = 0; k < 7; ++k) r.reserved[k] = 0.0;
+    r.n_hypotheses = g.rs[p].h1;  // hypotheses [0, h1) were sampled and solved
+    r.pad0 = 0;
+    for (int k = 0; k < 6; ++k) r.reserved[k] = 0.0;
     rec[p] = r;
 }
 

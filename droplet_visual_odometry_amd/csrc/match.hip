@@ -573,10 +573,14 @@ __global__ __launch_bounds__(256) void knn_pack_u8_kernel(const float* __restric
 #define DVO_KNN_U8Q 2
 #endif
 constexpr int kKnnU8Q = DVO_KNN_U8Q;  // queries per thread in knn_u8_kernel
+// Queries per workgroup the train split is sized for.  The byte kernel runs
+// 256 * kKnnU8Q = 512 per workgroup, but sizing the split for 512 (twice the
+// ranges) left its time unchanged (59 / 30 us at 5000^2 / 2000^2) and slowed
+// the merge (7.3 -> 10.8 us): profiles/r02_qb{256,512}_knn_kernel_stats.csv.
 #ifndef DVO_KNN_RANGE_QB
-#define DVO_KNN_RANGE_QB (256 * DVO_KNN_U8Q)
+#define DVO_KNN_RANGE_QB 256
 #endif
-constexpr int kKnnRangeQB = DVO_KNN_RANGE_QB;  // queries per workgroup the train split is sized for
+constexpr int kKnnRangeQB = DVO_KNN_RANGE_QB;
 
 template <int D, int NORM, int K>
 __global__ __launch_bounds__(256) void knn_u8_kernel(const uint32_t* __restrict__ q, const uint32_t* __restrict__ qn,
@@ -781,9 +785,8 @@ hipError_t launch_knn_k(int k, const float* d_q, int nq, const float* d_t, int n
 }  // namespace
 
 int knn_ranges(int nq, int nt, int cus) {
-    // about two rounds of resident workgroups of the byte kernel (knn_u8_kernel,
-    // the path every SIFT call takes: kKnnRangeQB queries per workgroup), at
-    // least 16 trains per range; the float kernel shares the split
+    // about two rounds of resident workgroups of kKnnRangeQB queries, at least
+    // 16 trains per range; the float and byte kernels share the split
     const int qblocks = (nq + kKnnRangeQB - 1) / kKnnRangeQB;
     int ranges = (cus * kKnnWgPerCu * 2) / qblocks;
     ranges = std::min(ranges, (nt + 15) / 16);

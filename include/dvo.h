@@ -160,7 +160,9 @@ typedef struct {
     double E[9];
     int32_t n_kp_prev, n_kp_cur, n_matches, n_inliers;
     int32_t n_good, ransac_iters, status, n_models;
-    double reserved[7];
+    int32_t n_hypotheses;  /* 5-point samples solved on the device (>= ransac_iters: rounds overshoot) */
+    int32_t pad0;
+    double reserved[6];
 } dvo_pair_record;
 
 int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** out);
