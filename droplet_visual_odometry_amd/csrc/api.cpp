@@ -938,6 +938,63 @@ int dvo_test_update_num_iters(dvo_ctx* ctx, double p, const double* ep, int n, i
     return DVO_OK;
 }
 
+int dvo_test_ransac_subsets(dvo_ctx* ctx, int m, int n, int32_t* idx) {
+    if (!ctx || !idx || m < 6 || n < 1) return DVO_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *drs, *dsub;
+    int rc;
+    if ((rc = scratch(ctx, 19, sizeof(RansacState), &drs)) || (rc = scratch(ctx, 18, (size_t)n * 20, &dsub))) return rc;
+    RansacState S{};
+    S.rng = ~0ull;
+    S.m = m;
+    S.niters = n;  // round 2 of the sampler covers [h1, niters) = [0, n)
+    HIP_TRY(hipMemcpyAsync(drs, &S, sizeof(S), hipMemcpyHostToDevice, ctx->stream));
+    GeomArgs g{};
+    g.rs = (RansacState*)drs;
+    g.subsets = (int32_t*)dsub;
+    g.hyp_cap = n;
+    g.m_const = m;
+    HIP_TRY(launch_test_ransac_sample(g, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(idx, dsub, (size_t)n * 20, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return DVO_OK;
+}
+
+int dvo_test_ransac_replay(dvo_ctx* ctx, const int32_t* nmod, const int32_t* cnt, int n, int m, double prob,
+                           int max_iters, int32_t* out) {
+    if (!ctx || !nmod || !cnt || !out || n < 1 || m < 6) return DVO_EINVAL;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *drs, *dn, *dc;
+    int rc;
+    if ((rc = scratch(ctx, 19, sizeof(RansacState), &drs)) || (rc = scratch(ctx, 16, (size_t)n * 4, &dn)) ||
+        (rc = scratch(ctx, 17, (size_t)n * 40, &dc)))
+        return rc;
+    RansacState S{};
+    S.m = m;
+    S.niters = max_iters > 1 ? max_iters : 1;
+    S.h0 = 0;
+    S.h1 = n < S.niters ? n : S.niters;
+    S.best_h = S.best_i = -1;
+    HIP_TRY(hipMemcpyAsync(drs, &S, sizeof(S), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dn, nmod, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dc, cnt, (size_t)n * 40, hipMemcpyHostToDevice, ctx->stream));
+    GeomArgs g{};
+    g.rs = (RansacState*)drs;
+    g.nmod = (int32_t*)dn;
+    g.cnt = (int32_t*)dc;
+    g.hyp_cap = n;
+    g.prob = prob;
+    HIP_TRY(launch_test_ransac_replay(g, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(&S, drs, sizeof(S), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    out[0] = S.iter;
+    out[1] = S.niters;
+    out[2] = S.maxgood;
+    out[3] = S.best_h;
+    out[4] = S.best_i;
+    return DVO_OK;
+}
+
 int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double* models, int* n) {
     if (!ctx || !q1 || !q2 || !models || !n) return DVO_EINVAL;
     HIP_TRY(hipSetDevice(ctx->device));

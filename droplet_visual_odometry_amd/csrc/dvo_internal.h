@@ -236,6 +236,8 @@ hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* 
                                    int* d_k, hipStream_t s);
 hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int model_points, int max_iters,
                                         int32_t* d_out, hipStream_t s);
+hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s);
+hipError_t launch_test_ransac_replay(const GeomArgs& g, hipStream_t s);
 hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n, hipStream_t s);
 
 }  // namespace dvo

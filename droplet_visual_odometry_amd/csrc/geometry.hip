@@ -982,9 +982,20 @@ constexpr int kSolveNT = 64;
 #endif
 constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 
+// getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
+// one wave per pair: idx[i] = rng.uniform(0, m) = rng.next() % m, redrawn
+// while it repeats an earlier index of the subset.  The MWC stream itself is
+// sequential (lane 0 runs it into LDS, one v_mad_u64_u32 per state), the
+// subsets are assembled 64 at a time: lane j takes the 5 states after the
+// 5j consumed before it, which is exact unless an earlier lane drew a
+// duplicate; the first such lane redoes its subset with the rejection loop
+// (wave-uniform, ~1% of subsets) and the next 64 start after it.
+constexpr int kSampleBuf = 1024;  // MWC states staged per refill
 __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round) {
-    const int p = blockIdx.x * 64 + threadIdx.x;
+    const int p = blockIdx.x;
     if (p >= pairs) return;
+    const int lane = threadIdx.x;
+    __shared__ uint64_t s_st[kSampleBuf];
     RansacState S = g.rs[p];
     int32_t* idx = g.subsets + (int64_t)p * g.hyp_cap * 5;
     int h0, h1;
@@ -999,7 +1010,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
         if (S.m < 5) {
             h1 = 0;
         } else if (S.m == 5) {  // count == modelPoints: one direct solve, no RANSAC
-            for (int i = 0; i < 5; ++i) idx[i] = i;
+            if (lane < 5) idx[lane] = lane;
             h1 = 1;
         } else {
             h1 = min(kRansacRound1, S.niters);
@@ -1007,7 +1018,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
         if (S.m <= 5) {
             S.h0 = h0;
             S.h1 = h1;
-            g.rs[p] = S;
+            if (lane == 0) g.rs[p] = S;
             return;
         }
     } else {
@@ -1017,23 +1028,74 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
     const unsigned m = (unsigned)S.m;
     // x % m by Lemire's fastmod (exact for every 32-bit x and m)
     const uint64_t M = ~0ull / m + 1;
-    Rng rng{S.rng};
-    for (int h = h0; h < h1; ++h) {  // getSubset: 5 distinct indices, rng.uniform(0, count)
-        int v[5];
-        for (int i = 0; i < 5; ++i) {
-            for (;;) {
-                v[i] = (int)__umul64hi(M * (uint64_t)rng.next(), (uint64_t)m);
-                bool dup = false;
-                for (int j = 0; j < i; ++j) dup |= v[j] == v[i];
-                if (!dup) break;
+    auto draw = [&](uint64_t st) { return (int)__umul64hi(M * (uint64_t)(uint32_t)st, (uint64_t)m); };
+    uint64_t gen = S.rng;   // last generated state (lane 0's stream position)
+    uint64_t last = S.rng;  // state after the last consumed draw
+    int avail = 0, cur = 0;
+    auto refill = [&]() {  // keep the unconsumed states, then extend the buffer to kSampleBuf
+        const int keep = avail - cur;
+        uint64_t tmp[kSampleBuf / 64];
+#pragma unroll
+        for (int k = 0; k < kSampleBuf / 64; ++k) tmp[k] = 64 * k + lane < keep ? s_st[cur + 64 * k + lane] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSampleBuf / 64; ++k)
+            if (64 * k + lane < keep) s_st[64 * k + lane] = tmp[k];
+        if (lane == 0) {
+            uint64_t st = gen;
+            for (int k = keep; k < kSampleBuf; ++k) {
+                st = (uint64_t)(uint32_t)st * 4164903690U + (st >> 32);
+                s_st[k] = st;
             }
-            idx[(int64_t)h * 5 + i] = v[i];
+        }
+        __syncthreads();
+        gen = s_st[kSampleBuf - 1];
+        avail = kSampleBuf;
+        cur = 0;
+    };
+    int h = h0;
+    while (h < h1) {
+        if (avail - cur < 5 * 64) refill();
+        const int hj = h + lane;
+        const bool act = hj < h1;
+        int v[5];
+        bool dup = false;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            v[i] = draw(s_st[cur + 5 * lane + i]);
+#pragma unroll
+            for (int j = 0; j < i; ++j) dup |= v[j] == v[i];
+        }
+        const unsigned long long bad = __ballot(act && dup);
+        const int nact = min(64, h1 - h);
+        const int nok = bad ? min(nact, (int)__builtin_ctzll(bad)) : nact;
+        if (lane < nok) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) idx[(int64_t)hj * 5 + i] = v[i];
+        }
+        if (nok > 0) last = s_st[cur + 5 * nok - 1];
+        h += nok;
+        cur += 5 * nok;
+        if (nok < nact) {  // hypothesis h drew a duplicate: its subset with the rejection loop (wave-uniform)
+            int w[5];
+            for (int i = 0; i < 5; ++i) {
+                for (;;) {
+                    if (cur == avail) refill();
+                    last = s_st[cur++];
+                    w[i] = draw(last);
+                    bool d = false;
+                    for (int j = 0; j < i; ++j) d |= w[j] == w[i];
+                    if (!d) break;
+                }
+            }
+            if (lane < 5) idx[(int64_t)h * 5 + lane] = w[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : lane == 3 ? 3 : 4];
+            ++h;
         }
     }
-    S.rng = rng.state;
+    S.rng = last;
     S.h0 = h0;
     S.h1 = h1;
-    g.rs[p] = S;
+    if (lane == 0) g.rs[p] = S;
 }
 
 __device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
@@ -1246,8 +1308,18 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
 }
 
 // The sequential bookkeeping of RANSACPointSetRegistrator::run over this
-// round's hypotheses, in order (counts staged through LDS, thread 0 replays).
-constexpr int kReplayNT = 64, kReplayMax = 1024;
+// round's hypotheses, in order:
+//   for each hypothesis while iter < niters: for each of its models:
+//     if count > max(maxgood, 4): best = it, maxgood = count,
+//                                 niters = RANSACUpdateNumIters(p, (m - count) / m, 5, niters)
+// A model can only change the state when its count beats the running maximum
+// of every count before it (and 4), so the wave finds those events in
+// parallel (a block of hypotheses per lane, an exclusive prefix max across
+// lanes) and lane 0 replays only the events, in order, with the stop rule:
+// nothing changes niters between events, so the loop ends at the first
+// hypothesis at or past niters.  Identical to the per-hypothesis loop
+// (which remains for rounds with more events than the event list holds).
+constexpr int kReplayNT = 64, kReplayMax = 1024, kReplayEv = 256;
 __global__ __launch_bounds__(kReplayNT) void ransac_replay_kernel(GeomArgs g) {
     const int p = blockIdx.x;
     RansacState* Sp = g.rs + p;
@@ -1255,32 +1327,101 @@ __global__ __launch_bounds__(kReplayNT) void ransac_replay_kernel(GeomArgs g) {
     if (Sp->m <= 5 || h1 <= h0) return;
     __shared__ int s_nmod[kReplayMax];
     __shared__ int s_cnt[kReplayMax * 10];
+    __shared__ int s_ev[kReplayEv];  // events: h << 4 | model
+    __shared__ RansacState s_S;      // the state between chunks
+    const int lane = threadIdx.x;
     const int64_t base = (int64_t)p * g.hyp_cap;
+    if (lane == 0) s_S = *Sp;
     for (int h0c = h0; h0c < h1; h0c += kReplayMax) {  // hyp_cap > kReplayMax: chunked
         const int hn = min(kReplayMax, h1 - h0c);
         __syncthreads();
-        for (int e = threadIdx.x; e < hn; e += kReplayNT) s_nmod[e] = g.nmod[base + h0c + e];
-        for (int e = threadIdx.x; e < hn * 10; e += kReplayNT) s_cnt[e] = g.cnt[(base + h0c) * 10 + e];
+        for (int e = lane; e < hn; e += kReplayNT) s_nmod[e] = g.nmod[base + h0c + e];
+        for (int e = lane; e < hn * 10; e += kReplayNT) s_cnt[e] = g.cnt[(base + h0c) * 10 + e];
         __syncthreads();
-        if (threadIdx.x == 0) {
-            RansacState S = *Sp;
-            const int m = S.m;
-            int it = S.iter, niters = S.niters, maxgood = S.maxgood;
-            for (int h = 0; h < hn && it < niters; ++h, ++it) {
-                for (int i = 0; i < s_nmod[h]; ++i) {
-                    const int good = s_cnt[h * 10 + i];
-                    if (good > (maxgood > 4 ? maxgood : 4)) {
-                        S.best_h = h0c + h;
-                        S.best_i = i;
-                        maxgood = good;
-                        niters = ransac_update_num_iters(g.prob, (double)(m - good) / m, 5, niters);
-                    }
+        const RansacState S = s_S;
+        // lane's contiguous block of hypotheses, its max count, exclusive prefix max over lanes
+        const int per = (hn + kReplayNT - 1) / kReplayNT;
+        const int b0 = min(hn, lane * per), b1 = min(hn, b0 + per);
+        int bmax = 0;
+        for (int h = b0; h < b1; ++h)
+            for (int i = 0; i < s_nmod[h]; ++i) bmax = max(bmax, s_cnt[h * 10 + i]);
+        int pre = bmax;  // inclusive scan, then shift
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(pre, o);
+            if (lane >= o) pre = max(pre, t);
+        }
+        int excl = __shfl_up(pre, 1);  // (shuffles stay in wave-uniform control flow)
+        if (lane == 0) excl = 0;
+        excl = max(excl, max(S.maxgood, 4));
+        int run = excl;
+        int nev = 0;
+        for (int h = b0; h < b1; ++h)
+            for (int i = 0; i < s_nmod[h]; ++i) {
+                const int c = s_cnt[h * 10 + i];
+                if (c > run) {
+                    run = c;
+                    ++nev;
                 }
             }
-            S.iter = it;
-            S.niters = niters;
-            S.maxgood = maxgood;
-            *Sp = S;
+        int off = nev;  // exclusive prefix sum of the event counts
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(off, o);
+            if (lane >= o) off += t;
+        }
+        const int total = __shfl(off, 63);
+        off -= nev;
+        if (total <= kReplayEv && nev > 0) {
+            run = excl;
+            for (int h = b0; h < b1; ++h)
+                for (int i = 0; i < s_nmod[h]; ++i) {
+                    const int c = s_cnt[h * 10 + i];
+                    if (c > run) {
+                        run = c;
+                        s_ev[off++] = h << 4 | i;
+                    }
+                }
+        }
+        __syncthreads();
+        if (lane == 0) {
+            const int m = S.m;
+            RansacState T = S;
+            int niters = S.niters, maxgood = S.maxgood;
+            int hdone = 0;  // hypotheses of this chunk processed
+            if (total <= kReplayEv) {
+                for (int e = 0; e < total; ++e) {
+                    const int h = s_ev[e] >> 4, i = s_ev[e] & 15;
+                    // niters is checked when a hypothesis starts, not between its models
+                    if (h + 1 != hdone && S.iter + h >= niters) break;  // the loop ends before hypothesis h
+                    const int good = s_cnt[h * 10 + i];
+                    T.best_h = h0c + h;
+                    T.best_i = i;
+                    maxgood = good;
+                    niters = ransac_update_num_iters(g.prob, (double)(m - good) / m, 5, niters);
+                    hdone = h + 1;
+                }
+                hdone = max(hdone, min(hn, niters - S.iter));
+            } else {
+                int it = S.iter;
+                for (int h = 0; h < hn && it < niters; ++h, ++it) {
+                    for (int i = 0; i < s_nmod[h]; ++i) {
+                        const int good = s_cnt[h * 10 + i];
+                        if (good > (maxgood > 4 ? maxgood : 4)) {
+                            T.best_h = h0c + h;
+                            T.best_i = i;
+                            maxgood = good;
+                            niters = ransac_update_num_iters(g.prob, (double)(m - good) / m, 5, niters);
+                        }
+                    }
+                }
+                hdone = it - S.iter;
+            }
+            T.iter = S.iter + hdone;
+            T.niters = niters;
+            T.maxgood = maxgood;
+            s_S = T;
+            *Sp = T;
         }
     }
 }
@@ -1341,7 +1482,7 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
     for (int round = 0; round < 2; ++round) {
         const int span = round == 0 ? min(kRansacRound1, cap) : cap - kRansacRound1;
         if (span <= 0) break;
-        hipLaunchKernelGGL(ransac_sample_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs, round);
+        hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, pairs, round);
         const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
         hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
         hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
@@ -1792,6 +1933,17 @@ hipError_t launch_pose_chain(const double* T_rel, int n, double* T_carry, double
     a.T_rel = const_cast<double*>(T_rel);
     a.T_abs = T_abs;
     hipLaunchKernelGGL(pose_chain_kernel, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+// Test hooks: the sampler / replay kernels on one pair whose RansacState the
+// caller set (api.cpp dvo_test_ransac_*).
+hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s) {
+    hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, s, g, 1, 1);
+    return hipGetLastError();
+}
+hipError_t launch_test_ransac_replay(const GeomArgs& g, hipStream_t s) {
+    hipLaunchKernelGGL(ransac_replay_kernel, dim3(1), dim3(kReplayNT), 0, s, g);
     return hipGetLastError();
 }
 

@@ -157,6 +157,25 @@ def test_update_num_iters(p, eps, model_points, max_iters, ctx=None):
     return out[:len(eps)]
 
 
+def test_ransac_subsets(m, n, ctx=None):
+    """Device getSubset draws for n hypotheses over m correspondences (n x 5)."""
+    c = _ctx(ctx)
+    idx = np.zeros((n, 5), np.int32)
+    c.check(c.lib.dvo_test_ransac_subsets(c.h, int(m), int(n), ptr(idx)))
+    return idx
+
+
+def test_ransac_replay(nmod, cnt, m, prob=0.999, max_iters=1000, ctx=None):
+    """Device RANSAC bookkeeping: (iterations, niters, max good, best h, best model)."""
+    c = _ctx(ctx)
+    nmod = np.ascontiguousarray(nmod, np.int32)
+    cnt = np.ascontiguousarray(cnt, np.int32).reshape(-1, 10)
+    out = np.zeros(5, np.int32)
+    c.check(c.lib.dvo_test_ransac_replay(c.h, ptr(nmod), ptr(cnt), len(nmod), int(m), float(prob), int(max_iters),
+                                         ptr(out)))
+    return tuple(int(v) for v in out)
+
+
 def test_five_point(q1, q2, ctx=None):
     c = _ctx(ctx)
     q1 = np.ascontiguousarray(q1, np.float64).reshape(10)

@@ -229,6 +229,14 @@ int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, i
 /* RANSACUpdateNumIters on the device for a batch of (ep) values. */
 int dvo_test_update_num_iters(dvo_ctx* ctx, double p, const double* ep, int n, int model_points, int max_iters,
                               int32_t* out);
+/* findEssentialMat's RANSAC sampler (getSubset with cv::RNG((uint64)-1)) for
+ * one pair of m >= 6 correspondences: idx gets n x 5 indices. */
+int dvo_test_ransac_subsets(dvo_ctx* ctx, int m, int n, int32_t* idx);
+/* The RANSAC bookkeeping (best model / niters / stop) over n hypotheses'
+ * model counts (nmod: n, cnt: n x 10); out = {iterations, niters, max good,
+ * best hypothesis, best model}. */
+int dvo_test_ransac_replay(dvo_ctx* ctx, const int32_t* nmod, const int32_t* cnt, int n, int m, double prob,
+                           int max_iters, int32_t* out);
 /* 5-point kernel on one sample of 5 normalised correspondences. */
 int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double* models, int* n);
 

@@ -682,6 +682,48 @@ int ora_find_essential(const double* p1, const double* p2, int m, const double* 
     return 0;
 }
 
+// The subsets ora_find_essential draws: getSubset (ptsetreg.cpp) with
+// cv::RNG((uint64)-1), n hypotheses of 5 distinct indices in [0, m).
+int ora_ransac_subsets(int m, int n, int32_t* idx) {
+    if (m < 6 || n < 0) return -1;
+    Rng rng((uint64_t)(int64_t)-1);
+    for (int h = 0; h < n; ++h)
+        for (int i = 0; i < 5; ++i) {
+            for (;;) {
+                const int v = rng.uniform(0, m);
+                int j;
+                for (j = 0; j < i; ++j)
+                    if (v == idx[h * 5 + j]) break;
+                idx[h * 5 + i] = v;
+                if (j == i) break;
+            }
+        }
+    return 0;
+}
+
+// The bookkeeping of RANSACPointSetRegistrator::run (the loop of
+// ora_find_essential) over given per-hypothesis model inlier counts:
+// out = {iterations run, final niters, max good, best hypothesis, best model}.
+int ora_ransac_replay(const int32_t* nmod, const int32_t* cnt, int n, int m, double prob, int max_iters, int32_t* out) {
+    int niters = std::max(max_iters, 1), max_good = 0, best_h = -1, best_i = -1, iter;
+    for (iter = 0; iter < niters && iter < n; iter++)
+        for (int i = 0; i < nmod[iter]; ++i) {
+            const int good = cnt[iter * 10 + i];
+            if (good > std::max(max_good, 4)) {
+                max_good = good;
+                best_h = iter;
+                best_i = i;
+                niters = ransac_update_num_iters(prob, (double)(m - good) / m, 5, niters);
+            }
+        }
+    out[0] = iter;
+    out[1] = niters;
+    out[2] = max_good;
+    out[3] = best_h;
+    out[4] = best_i;
+    return 0;
+}
+
 int ora_recover_pose(const double* E, const double* p1, const double* p2, int m, const double* K, double dist_thresh,
                      const uint8_t* mask_in, double* R, double* t, uint8_t* mask_out, int* good_out) {
     std::vector<double> n1(2 * m), n2(2 * m);

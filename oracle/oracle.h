@@ -76,6 +76,11 @@ int ora_five_point(const double* p1, const double* p2, double* models, int* n);
 int ora_jacobi_svd(double* At, int m, int n, int n1, double* W, double* Vt);
 int ora_solve_poly(const double* coeffs, int n, int max_iters, double* roots /*2n*/);
 int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
+// RANSAC pieces pinned separately: getSubset's draws (n x 5) and the sequential
+// best / niters bookkeeping over per-hypothesis counts (cnt: n x 10);
+// out = {iterations, niters, max good, best hypothesis, best model}.
+int ora_ransac_subsets(int m, int n, int32_t* idx);
+int ora_ransac_replay(const int32_t* nmod, const int32_t* cnt, int n, int m, double prob, int max_iters, int32_t* out);
 
 /* Image pre-processing (undistort.cpp): cv::getOptimalNewCameraMatrix and
  * cv::undistort (striped initUndistortRectifyMap + remap INTER_LINEAR,

@@ -89,6 +89,8 @@ def lib():
             "ora_jacobi_svd": [_f64p, _c, _c, _c, _f64p, _f64p],
             "ora_solve_poly": [_f64p, _c, _c, _f64p],
             "ora_ransac_update_num_iters": [_d, _d, _c, _c],
+            "ora_ransac_subsets": [_c, _c, _i32p],
+            "ora_ransac_replay": [_i32p, _i32p, _c, _c, _d, _c, _i32p],
             "ora_get_optimal_new_camera_matrix": [_f64p, _f64p, _c, _c, _c, _d, _c, _c, _f64p],
             "ora_undistort": [_u8p, _c, _c, _c, _f64p, _f64p, _c, ctypes.c_void_p, _u8p, _c,
                               np.ctypeslib.ndpointer(np.int16, flags="C"), np.ctypeslib.ndpointer(np.uint16, flags="C")],
@@ -261,6 +263,20 @@ def solve_poly(coeffs, max_iters=300):
 
 def ransac_update_num_iters(p, ep, model_points, max_iters):
     return lib().ora_ransac_update_num_iters(p, ep, model_points, max_iters)
+
+
+def ransac_subsets(m, n):
+    idx = np.zeros((max(n, 1), 5), np.int32)
+    lib().ora_ransac_subsets(m, n, idx)
+    return idx[:n]
+
+
+def ransac_replay(nmod, cnt, m, prob=0.999, max_iters=1000):
+    nmod = np.ascontiguousarray(nmod, np.int32)
+    cnt = np.ascontiguousarray(cnt, np.int32).reshape(-1, 10)
+    out = np.zeros(5, np.int32)
+    lib().ora_ransac_replay(nmod, cnt, len(nmod), m, prob, max_iters, out)
+    return tuple(int(v) for v in out)
 
 
 def keypoints_to_points(kps):

@@ -243,3 +243,24 @@ def test_golden_pair_reproduces(oracle_mod):
     np.testing.assert_array_equal(r["R"], g["R"])
     np.testing.assert_array_equal(r["t_unit"], g["t_unit"])
     assert r["good"] == int(g["good"]) and r["iters"] == int(g["iters"])
+
+
+def test_oracle_subsets_follow_cv_rng(oracle_mod):
+    """getSubset's draws from cv::RNG((uint64)-1): state = (uint32)state *
+    4164903690 + (state >> 32), uniform(0, m) = (uint32)state % m, a draw
+    repeating an earlier index of the subset is redrawn."""
+    def ref(m, n):
+        st, out = (1 << 64) - 1, []
+        for _ in range(n):
+            v = []
+            for _ in range(5):
+                while True:
+                    st = ((st & 0xFFFFFFFF) * 4164903690 + (st >> 32)) & ((1 << 64) - 1)
+                    x = (st & 0xFFFFFFFF) % m
+                    if x not in v:
+                        break
+                v.append(x)
+            out.append(v)
+        return out
+    for m, n in [(6, 50), (9, 200), (871, 300)]:
+        assert oracle_mod.ransac_subsets(m, n).tolist() == ref(m, n)
