@@ -11,16 +11,28 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "dvo_internal.h"
 
 using namespace dvo;
 
+struct SiftPlanDev {  // per-size device buffers of dvo_sift_detect_and_compute
+    int w = 0, h = 0;
+    SiftArgs a{};
+    float* taps = nullptr;
+    int tap_off[6] = {0}, tap_n[6] = {0};
+    uint8_t* img = nullptr;
+    int pitch = 0;
+    std::vector<void*> allocs;
+};
+
 struct dvo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    SiftPlanDev sift;
     // grow-only scratch for the per-call entry points
     std::vector<std::pair<void*, size_t>> scratch;
     dvo_stream* call_stream = nullptr;  // cached plan for detectAndCompute
@@ -414,6 +426,7 @@ int dvo_ctx_create(dvo_ctx** out, int device) {
 void dvo_ctx_destroy(dvo_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
+    for (void* p : ctx->sift.allocs) hipFree(p);
     if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
     for (auto& e : ctx->scratch)
         if (e.first) hipFree(e.first);
@@ -741,6 +754,123 @@ int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int
     HIP_TRY(hipMemcpyAsync(dist, bd, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(train_idx, bi, out_n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return DVO_OK;
+}
+
+namespace {
+// getGaussianKernel(ksize = cvRound(sigma * 8 + 1) | 1, sigma, CV_32F), as oracle/sift.cpp gauss_kernel
+std::vector<float> sift_gauss_taps(double sigma) {
+    const int n = (int)std::nearbyint(sigma * 4 * 2 + 1) | 1;
+    std::vector<float> k(n);
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; ++i) {
+        const double x = i - (n - 1) * 0.5;
+        k[i] = (float)std::exp(scale2X * x * x);
+        sum += k[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
+    return k;
+}
+
+int sift_plan(dvo_ctx* ctx, int w, int h) {
+    SiftPlanDev& P = ctx->sift;
+    if (P.w == w && P.h == h) return DVO_OK;
+    for (void* p : P.allocs) hipFree(p);
+    P = SiftPlanDev{};
+    SiftArgs& A = P.a;
+    const int W = 2 * w, H = 2 * h;  // firstOctave = -1
+    A.noct = (int)std::nearbyint(std::log((double)std::min(W, H)) / std::log(2.) - 2) + 1;
+    A.noct = std::max(1, std::min(A.noct, kSiftMaxOct));
+    int64_t gp = 0, dg = 0;
+    for (int o = 0; o < A.noct; ++o) {
+        A.ow[o] = o == 0 ? W : A.ow[o - 1] / 2;
+        A.oh[o] = o == 0 ? H : A.oh[o - 1] / 2;
+        if (A.ow[o] < 1 || A.oh[o] < 1) {  // as small as the pyramid goes
+            A.noct = o;
+            break;
+        }
+        const int64_t px = (int64_t)A.ow[o] * A.oh[o];
+        for (int l = 0; l < 6; ++l) A.gp_off[o * 6 + l] = gp + l * px;
+        for (int l = 0; l < 5; ++l) A.dog_off[o * 5 + l] = dg + l * px;
+        gp += 6 * px;
+        dg += 5 * px;
+    }
+    A.cand_cap = 1 << 18;
+    A.kp_cap = 1 << 16;
+    std::vector<float> taps;
+    const double sig0 = std::sqrt(std::max(1.6f * 1.6f - 0.5f * 0.5f * 4, 0.01f));
+    std::vector<double> sig(6);
+    sig[0] = sig0;
+    const double k = std::pow(2., 1. / 3);
+    for (int i = 1; i < 6; ++i) {
+        const double sig_prev = std::pow(k, (double)(i - 1)) * 1.6f, sig_total = sig_prev * k;
+        sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
+    }
+    for (int i = 0; i < 6; ++i) {
+        const std::vector<float> t = sift_gauss_taps(i == 0 ? (double)(float)sig0 : sig[i]);
+        P.tap_off[i] = (int)taps.size();
+        P.tap_n[i] = (int)t.size();
+        taps.insert(taps.end(), t.begin(), t.end());
+    }
+    P.pitch = (w + 255) & ~255;
+    auto A_ = [&](auto*& p, size_t bytes) {
+        void* q = nullptr;
+        if (hipMalloc(&q, bytes ? bytes : 16) != hipSuccess) return false;
+        P.allocs.push_back(q);
+        p = static_cast<std::remove_reference_t<decltype(p)>>(q);
+        return true;
+    };
+    int order_n = 1;
+    while (order_n < A.kp_cap) order_n <<= 1;
+    int* counters = nullptr;
+    if (!A_(A.gp, (size_t)gp * 4) || !A_(A.dog, (size_t)dg * 4) || !A_(A.tmp, (size_t)W * H * 4) ||
+        !A_(A.cand, (size_t)A.cand_cap * sizeof(int4)) || !A_(A.raw, (size_t)A.kp_cap * sizeof(dvo_keypoint)) ||
+        !A_(A.order, (size_t)order_n * 4) || !A_(A.kps, (size_t)A.kp_cap * sizeof(dvo_keypoint)) ||
+        !A_(A.desc, (size_t)A.kp_cap * 128 * 4) || !A_(counters, 64) || !A_(P.taps, taps.size() * 4) ||
+        !A_(P.img, (size_t)P.pitch * h)) {
+        for (void* p : P.allocs) hipFree(p);
+        P = SiftPlanDev{};
+        return fail(ctx, DVO_EHIP, "SIFT buffers: hipMalloc failed");
+    }
+    A.ncand = counters;
+    A.nraw = counters + 1;
+    A.nkp = counters + 2;
+    A.flags = counters + 3;
+    if (hipMemcpy(P.taps, taps.data(), taps.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(ctx, DVO_EHIP, "SIFT taps upload failed");
+    P.w = w;
+    P.h = h;
+    return DVO_OK;
+}
+}  // namespace
+
+int dvo_sift_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, dvo_keypoint* kps,
+                                float* desc, int cap, int* n_out) {
+    if (!ctx || !n_out) return DVO_EINVAL;
+    *n_out = 0;
+    if (!img || stride < w) return fail(ctx, DVO_EINVAL, "bad image buffer");
+    if (w < 1 || h < 1 || w >= kMaxW || h >= kMaxW) return fail(ctx, DVO_EINVAL, "image size out of range (1..4095)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = sift_plan(ctx, w, h);
+    if (rc) return rc;
+    SiftPlanDev& P = ctx->sift;
+    HIP_TRY(hipMemsetAsync(P.a.ncand, 0, 16, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(P.img, P.pitch, img, stride, w, h, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_sift(P.a, P.img, w, h, P.pitch, P.taps, P.tap_off, P.tap_n, ctx->stream));
+    int cnt[4];
+    HIP_TRY(hipMemcpyAsync(cnt, P.a.ncand, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (cnt[3]) return fail(ctx, DVO_ECAP, "SIFT: more extrema / keypoints than the device lists hold");
+    const int n = cnt[2];
+    *n_out = n;
+    if (n > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    if (n) {
+        if (kps) HIP_TRY(hipMemcpyAsync(kps, P.a.kps, (size_t)n * sizeof(dvo_keypoint), hipMemcpyDeviceToHost, ctx->stream));
+        if (desc) HIP_TRY(hipMemcpyAsync(desc, P.a.desc, (size_t)n * 128 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
     return DVO_OK;
 }
 

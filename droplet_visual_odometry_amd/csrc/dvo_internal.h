@@ -187,6 +187,32 @@ struct GeomArgs {
 
 constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;
 
+// SIFT_create().detectAndCompute of one image (sift.hip).  Octave o has
+// size ow[o] x oh[o] (octave 0 = the 2x upscaled input); its Gaussian layer l
+// (0..5) starts at gp + gp_off[o * 6 + l] and DoG layer l (0..4) at
+// dog + dog_off[o * 5 + l] (floats, rows of ow[o]).
+constexpr int kSiftMaxOct = 16;
+struct SiftArgs {
+    float* gp;
+    float* dog;
+    float* tmp;             // row-pass buffer, ow[0] * oh[0]
+    int64_t gp_off[kSiftMaxOct * 6];
+    int64_t dog_off[kSiftMaxOct * 5];
+    int ow[kSiftMaxOct], oh[kSiftMaxOct];
+    int noct;
+    int4* cand;             // (octave, layer, row, col) extrema
+    int* ncand;
+    int cand_cap;
+    dvo_keypoint* raw;      // refined, oriented keypoints (unsorted)
+    int* nraw;
+    int kp_cap;
+    int32_t* order;         // sort scratch, next power of two >= kp_cap
+    dvo_keypoint* kps;      // final keypoints (sorted, deduplicated, input-image units)
+    int* nkp;
+    float* desc;            // kp_cap x 128
+    int* flags;             // 1: candidate overflow, 2: keypoint overflow
+};
+
 // ---- host entry points of the kernels (implemented in the .hip files) -------
 // ev: optional table of 2*DVO_NSTAGES events recorded around each stage.
 inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
@@ -230,6 +256,9 @@ hipError_t launch_knn_float(const float* d_q, int nq, const float* d_t, int nt, 
 // One-pair Hamming match (dvo_bf_match_hamming) on the stream's MFMA matcher;
 // d_work: match_pair_work_size(nq, nt) bytes.  Output in queryIdx order.
 size_t match_pair_work_size(int nq, int nt);
+// d_taps: the 6 Gaussian kernels (initial blur, layers 1..5) back to back.
+hipError_t launch_sift(const SiftArgs& A, const uint8_t* d_img, int w, int h, int stride, const float* d_taps,
+                       const int* tap_off, const int* tap_n, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,

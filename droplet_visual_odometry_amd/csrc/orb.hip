@@ -55,6 +55,9 @@ constexpr int kCdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3}
 // (level ratio <= 1.5); wider ratios take a bytewise path.
 constexpr int kRsR = 4;
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
 __device__ __forceinline__ uint32_t byte_of(const uint32_t* w, int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
 
 __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l) {
@@ -193,25 +196,45 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int wb0 = min(i0[0] >> 2, kRsW - 3);  // lanes past the level's right edge: any in-range words
     const int base = 4 * wb0;
     const bool full = x0 + 4 <= D.w;
+    // Per-lane constants for all rows: the 8-byte source window starting at the
+    // lane's first tap (v_alignbyte of the 3 staged words), and per output
+    // pixel j a v_perm selector giving the u16 pair (src[o_j], src[o_j + 1])
+    // and the pair of weights (256 - c1, c1) for v_dot2_u32_u16.  The 4 taps of
+    // a lane span <= 6 bytes at ratio <= 1.25.
+    const int sh = min(i0[0] - base, 3);
+    uint32_t sel[4], kw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t r = (uint32_t)min(max(i0[j] - base - sh, 0), 6);
+        sel[j] = 0x0C000C00u | r | ((r + 1) << 16);
+        kw[j] = (uint32_t)(256 - c1[j]) | ((uint32_t)c1[j] << 16);
+    }
 #pragma unroll
     for (int rr = 0; rr < kRsLR; ++rr) {
         const int dy = dy0 + rr;
         if (dy >= D.h) break;
         const int lr = coef_ofs(cys[rr]) - sy0;
         const uint32_t cy1 = coef_c1(cys[rr]);
+        const uint32_t ky = (256u - cy1) | (cy1 << 16);
         const int lr1 = min(lr + 1, kRsLRows - 1);  // weight-0 row past the window: any in-range row
-        const uint32_t wa[3] = {tile[lr][wb0], tile[lr][wb0 + 1], tile[lr][wb0 + 2]};
-        const uint32_t wb[3] = {tile[lr1][wb0], tile[lr1][wb0 + 1], tile[lr1][wb0 + 2]};
-        uint32_t word = 0;
+        const uint32_t a0 = tile[lr][wb0], a1 = tile[lr][wb0 + 1], a2 = tile[lr][wb0 + 2];
+        const uint32_t b0 = tile[lr1][wb0], b1 = tile[lr1][wb0 + 1], b2 = tile[lr1][wb0 + 2];
+        const uint32_t alo = __builtin_amdgcn_alignbyte(a1, a0, sh), ahi = __builtin_amdgcn_alignbyte(a2, a1, sh);
+        const uint32_t blo = __builtin_amdgcn_alignbyte(b1, b0, sh), bhi = __builtin_amdgcn_alignbyte(b2, b1, sh);
+        uint32_t v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k1 = c1[j], k0 = 256 - k1;
-            const int o = min(i0[j] - base, 10);
-            const uint32_t h0 = k0 * byte_of(wa, o) + k1 * byte_of(wa, o + 1);
-            const uint32_t h1 = k0 * byte_of(wb, o) + k1 * byte_of(wb, o + 1);
-            const uint32_t v = (h0 * (256 - cy1) + h1 * cy1 + 32768u) >> 16;
-            word |= (v > 255 ? 255u : v) << (8 * j);
+            // h = (256 - c1) * s[o] + c1 * s[o + 1] <= 65280; then the rows: h0 (256 - cy1) + h1 cy1 + 2^15 < 2^24
+            const uint32_t h0 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(ahi, alo, sel[j])),
+                                                       as_u16x2(kw[j]), 0u, false);
+            const uint32_t h1 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(bhi, blo, sel[j])),
+                                                       as_u16x2(kw[j]), 0u, false);
+            v[j] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u)), as_u16x2(ky), 32768u,
+                                          false);
         }
+        // byte 2 of each sum (< 2^24, so it is (sum >> 16) <= 255)
+        const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[3], v[2], 0x0C0C0602u),
+                                                    __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0602u), 0x05040100u);
         uint8_t* drow = dst + (int64_t)dy * D.pitch;
         if (full) {
             *reinterpret_cast<uint32_t*>(drow + x0) = word;
@@ -237,8 +260,6 @@ __device__ __forceinline__ int refl101(int p, int n) {
     return p;
 }
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t dpp_from_left(uint32_t v) {  // lane i <- lane i-1 (wave_shr:1)
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
 }

@@ -5,7 +5,7 @@ The reference calls (scripts/visual_odometry_v3.py):
   cv.BFMatcher(normType=NORM_HAMMING, crossCheck=True)  :75    .match :219
   cv.BFMatcher(normType=NORM_L1) .match / .knnMatch(k=2) :99-106, :200-204, :214-215 (SIFT/SURF)
   cv.FlannBasedMatcher(index, search).knnMatch(k=2)     :206-212 (exact-search stand-in)
-  cv.xfeatures2d.SIFT_create() / SURF_create(400)       :100, :104 (host cv2 when importable)
+  cv.xfeatures2d.SIFT_create()                          :100 (GPU; SURF_create(400), :104, host cv2 contrib only)
   detector.detectAndCompute(img, None)                  :373
   cv.drawKeypoints(img, kps, None, color, flags=0)      :375   (result discarded, D6)
   cv.KeyPoint_convert(kps)                              :355, :358
@@ -488,18 +488,47 @@ def _host_cv2():
         return None
 
 
+class SIFT:
+    """cv2.SIFT with SIFT_create()'s defaults (v3:100), on the GPU
+    (dvo_sift_detect_and_compute): keypoints and float32[N, 128] descriptors
+    for the float k-NN matchers of the sift / knn_sift / flann modes."""
+
+    def __init__(self, nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10, sigma=1.6):
+        if (nfeatures != 0 or nOctaveLayers != 3 or not np.isclose(contrastThreshold, 0.04)
+                or not np.isclose(edgeThreshold, 10) or not np.isclose(sigma, 1.6)):
+            raise error("only the SIFT_create() defaults are implemented (the reference uses them, v3:100)")
+
+    def detectAndCompute(self, image, mask, descriptors=None, useProvidedKeypoints=False):
+        if mask is not None:
+            raise error("SIFT masks are not supported (the reference passes None, v3:373)")
+        if useProvidedKeypoints:
+            raise error("useProvidedKeypoints is not supported")
+        img = _gray(image)
+        try:
+            kps, desc = ops.sift_detect_and_compute(img)
+        except DVOError as e:
+            raise error(str(e)) from e
+        return KeyPoints(kps), (desc if len(kps) else None)
+
+    def detect(self, image, mask=None):
+        return self.detectAndCompute(image, mask)[0]
+
+    def descriptorSize(self):
+        return 128
+
+
+def SIFT_create(nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThreshold=10, sigma=1.6):
+    return SIFT(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma)
+
+
 class _XFeatures2d:
-    """SIFT / SURF detection (v3:100, :104) is CPU work in the reference and is
-    not on the accelerated path: these return the host cv2 detector when cv2
-    is importable (its descriptors then feed the GPU matchers above) and
-    raise cv.error otherwise."""
+    """cv2.xfeatures2d: SIFT on the GPU (v3:100); SURF (v3:104, patented,
+    contrib-only) is not implemented on the device and comes from a host cv2
+    contrib build when one is importable, else cv.error."""
 
     @staticmethod
     def SIFT_create(*a, **k):
-        cv2 = _host_cv2()
-        if cv2 is None:
-            raise error("SIFT detection needs the host cv2 package (not installed); matching is on the GPU")
-        return cv2.SIFT_create(*a, **k) if hasattr(cv2, "SIFT_create") else cv2.xfeatures2d.SIFT_create(*a, **k)
+        return SIFT_create(*a, **k)
 
     @staticmethod
     def SURF_create(*a, **k):

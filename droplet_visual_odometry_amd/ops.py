@@ -4,6 +4,7 @@ Each function replaces one OpenCV operator of the reference's hot path and
 mirrors its argument meaning, output layout and failure points:
 
   detect_and_compute   cv::ORB::detectAndCompute          visual_odometry_v3.py:373
+  sift_detect_and_compute  cv::SIFT::detectAndCompute    visual_odometry_v3.py:100, :373
   bf_match             cv::BFMatcher(NORM_HAMMING).match  visual_odometry_v3.py:75, :219
   bf_knn_float         cv::BFMatcher(NORM_L1).knnMatch / .match, FLANN knnMatch
                                                           visual_odometry_v3.py:99-106, :200-215
@@ -42,6 +43,28 @@ def detect_and_compute(img: np.ndarray, nfeatures: int = 500, fast_threshold: in
         n = ctypes.c_int()
         rc = c.lib.dvo_orb_detect_and_compute(c.h, ctypes.byref(prm), ptr(img), w, h, img.strides[0], ptr(kps),
                                               ptr(desc), cap, ctypes.byref(n))
+        if rc == DVO_ECAP and n.value > cap:
+            cap = n.value
+            continue
+        c.check(rc)
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def sift_detect_and_compute(img: np.ndarray, ctx=None):
+    """SIFT_create().detectAndCompute(img, None): keypoints (KEYPOINT_DTYPE, in
+    OpenCV's removeDuplicatedSorted order) and float32[N, 128] descriptors."""
+    c = _ctx(ctx)
+    img = np.ascontiguousarray(img)
+    if img.dtype != np.uint8 or img.ndim != 2:
+        raise DVOError(-1, "sift_detect_and_compute expects a mono8 image (uint8[H, W])")
+    h, w = img.shape
+    cap = 8192
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 128), np.float32)
+        n = ctypes.c_int()
+        rc = c.lib.dvo_sift_detect_and_compute(c.h, ptr(img), w, h, img.strides[0], ptr(kps), ptr(desc), cap,
+                                               ctypes.byref(n))
         if rc == DVO_ECAP and n.value > cap:
             cap = n.value
             continue

@@ -93,6 +93,15 @@ int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t*
 int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
                      int32_t* train_idx, float* dist);
 
+/* Replaces cv::xfeatures2d::SIFT_create().detectAndCompute(img, None) — the
+ * detector of the 'sift' / 'knn_sift' / 'flann' modes, visual_odometry_v3.py:100
+ * (construction) and :373 (call).  Default parameters (nfeatures 0, 3 octave
+ * layers, contrast 0.04, edge 10, sigma 1.6, input upscaled 2x).  img: host
+ * mono8.  kps: keypoints in OpenCV's removeDuplicatedSorted order; desc: n x
+ * 128 floats (integer values 0..255).  *n_out = count (DVO_ECAP if > cap). */
+int dvo_sift_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, dvo_keypoint* kps,
+                                float* desc, int cap, int* n_out);
+
 /* Replaces cv::findEssentialMat(points1, points2, K, RANSAC, prob, threshold,
  * maxIters) — visual_odometry_v3.py:297-300.  p1/p2: m x 2 doubles (pixel
  * coords, the float32 KeyPoint_convert output widened).  E receives 3 rows

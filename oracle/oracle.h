@@ -82,6 +82,12 @@ int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_i
 int ora_ransac_subsets(int m, int n, int32_t* idx);
 int ora_ransac_replay(const int32_t* nmod, const int32_t* cnt, int n, int m, double prob, int max_iters, int32_t* out);
 
+// ---- SIFT_create().detectAndCompute (sift.cpp; the 'sift' / 'knn_sift' /
+// 'flann' modes, visual_odometry_v3.py:99-103, :373).  kps sorted as
+// removeDuplicatedSorted leaves them; desc: n x 128 floats (integer values).
+int ora_sift_detect_and_compute(const uint8_t* img, int w, int h, int stride, ora_keypoint* kps, float* desc, int cap,
+                                int* n_out);
+
 /* Image pre-processing (undistort.cpp): cv::getOptimalNewCameraMatrix and
  * cv::undistort (striped initUndistortRectifyMap + remap INTER_LINEAR,
  * BORDER_CONSTANT).  xy / frac receive the 16SC2 / 16UC1 maps (w*h). */

@@ -91,6 +91,7 @@ def lib():
             "ora_ransac_update_num_iters": [_d, _d, _c, _c],
             "ora_ransac_subsets": [_c, _c, _i32p],
             "ora_ransac_replay": [_i32p, _i32p, _c, _c, _d, _c, _i32p],
+            "ora_sift_detect_and_compute": [_u8p, _c, _c, _c, _kpp, _f32p, _c, _ip],
             "ora_get_optimal_new_camera_matrix": [_f64p, _f64p, _c, _c, _c, _d, _c, _c, _f64p],
             "ora_undistort": [_u8p, _c, _c, _c, _f64p, _f64p, _c, ctypes.c_void_p, _u8p, _c,
                               np.ctypeslib.ndpointer(np.int16, flags="C"), np.ctypeslib.ndpointer(np.uint16, flags="C")],
@@ -159,6 +160,22 @@ def detect_and_compute(img, nfeatures=500):
     rc = lib().ora_orb_detect_and_compute(img, w, h, w, nfeatures, kps, desc, cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def sift_detect_and_compute(img):
+    """SIFT_create().detectAndCompute(img, None): (KEYPOINT_DTYPE array, float32[n, 128])."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = 4096
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 128), np.float32)
+        n = ctypes.c_int()
+        rc = lib().ora_sift_detect_and_compute(img, w, h, w, kps, desc, cap, ctypes.byref(n))
+        if rc == -5:
+            cap = n.value
+            continue
+        return kps[:n.value].copy(), desc[:n.value].copy()
 
 
 def bf_match(dq, dt, mode=1):
