@@ -142,16 +142,32 @@ __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l
 constexpr int kRsLR = 8;  // output rows per wave (32 per workgroup)
 constexpr int kRsW = 96, kRsLRows = 44;  // 32 * 1.25 + 2 source rows, padded to a multiple of 4
 
-__global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l) {
+// 1-D grids of (frame, item) blocks, XCD-grouped: workgroups are dispatched
+// round-robin over the 8 XCDs (block b on XCD b & 7), so XCD x takes frames
+// x, x + 8, ... and one frame's items run on one XCD at about the same time.
+// Neighbouring tiles / strips share the 128-B lines of their halo columns
+// through that XCD's L2 instead of each XCD fetching its own copy.
+// Grid: nitems * xcd_frames(F) blocks; blocks past the last frame return.
+__host__ __device__ constexpr int xcd_frames(int F) { return (F + 7) & ~7; }
+__device__ __forceinline__ int xcd_frame_item(int nitems, int& item) {
+    const int q8 = blockIdx.x >> 3, fq = q8 / nitems;
+    item = q8 - fq * nitems;
+    return (blockIdx.x & 7) + 8 * fq;
+}
+
+__global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l, int gx) {
     __shared__ uint32_t tile[kRsLRows][kRsW];
-    const int f = blockIdx.z;
+    int item;
+    const int f = xcd_frame_item(gx * ((P.plan.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)), item);
+    if (f >= P.nframes) return;
+    const int by = item / gx, bxi = item - by * gx;
     const LevelGeom& S = P.plan.L[l - 1];
     const LevelGeom& D = P.plan.L[l];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int xa = blockIdx.x * 256;
+    const int xa = bxi * 256;
     const int x0 = xa + 4 * lane;
-    const int ty0 = blockIdx.y * (4 * kRsLR);
+    const int ty0 = by * (4 * kRsLR);
     const uint8_t* src = level_ptr(P, f, l - 1);
     const int sp = level_pitch(P, l - 1);
     uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
@@ -347,8 +363,9 @@ __device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int s
 }
 
 __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
-    const int f = blockIdx.y;
-    const int item = blockIdx.x;
+    int item;
+    const int f = xcd_frame_item(P.plan.total_tiles, item);
+    if (f >= P.nframes) return;
     int l = 0;
     while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].tile_base) ++l;
     const LevelGeom& G = P.plan.L[l];
@@ -509,8 +526,9 @@ __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int 
 }
 
 __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
-    const int f = blockIdx.y;
-    const int strip = blockIdx.x;
+    int strip;
+    const int f = xcd_frame_item(P.plan.total_strips, strip);
+    if (f >= P.nframes) return;
     int l = 0;
     while (l + 1 < P.plan.nlevels && strip >= P.plan.L[l + 1].strip_base) ++l;
     const LevelGeom& G = P.plan.L[l];
@@ -1352,20 +1370,20 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
         const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
         if (lds)
             hipLaunchKernelGGL(resize_level_lds_kernel,
-                               dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR), F), dim3(256), 0,
-                               s, P, l);
+                               dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) * xcd_frames(F)),
+                               dim3(256), 0, s, P, l, (pl.L[l].w + 255) / 256);
         else  // level pairs whose rounded sizes differ by more than 1.25x: tiny frames (8x8: levels 4->5, 6->7)
             hipLaunchKernelGGL(resize_level_kernel, dim3((pl.L[l].w + 255) / 256, (pl.L[l].h + 4 * kRsR - 1) / (4 * kRsR), F),
                                dim3(256), 0, s, P, l);
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
-    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles, F), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
     if (pl.total_strips > 0)
-        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips, F), dim3(kFastNT), 0, s, P);
+        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);

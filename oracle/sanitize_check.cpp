@@ -119,6 +119,28 @@ int main() {
     double X[16];
     EXPECT(ora_triangulate(P1, P2, x1, x2, 4, X) == 0);
 
+    // RANSAC parts: the sampler past one 1024-state chunk, the replay
+    {
+        std::vector<int32_t> sub(5 * 300);
+        EXPECT(ora_ransac_subsets(m > 5 ? m : 6, 300, sub.data()) == 0);
+        std::vector<int32_t> nmod(4096), cnt(4096 * 10), out(8);  // counts: 10 slots per hypothesis
+        for (int i = 0; i < 4096; ++i) nmod[i] = 1 + (int)(rng() % 3);
+        for (auto& c : cnt) c = (int)(rng() % 200);
+        ora_ransac_replay(nmod.data(), cnt.data(), 4096, 200, 0.999, 4096, out.data());
+        ora_ransac_replay(nmod.data(), cnt.data(), 0, 200, 0.999, 1000, out.data());
+    }
+
+    // SIFT, textured and blank
+    {
+        std::vector<ora_keypoint> sk(4000);
+        std::vector<float> sd(4000 * 128);
+        int ns = 0;
+        EXPECT(ora_sift_detect_and_compute(a.data(), W, H, W, sk.data(), sd.data(), 4000, &ns) == 0 && ns > 0);
+        std::vector<uint8_t> flat((size_t)64 * 48, 90);
+        ora_sift_detect_and_compute(flat.data(), 64, 48, 64, sk.data(), sd.data(), 4000, &ns);
+        ora_sift_detect_and_compute(a.data(), W, H, W, sk.data(), sd.data(), 3, &ns);  // cap below the count
+    }
+
     // pre-processing
     const double dist5[5] = {0.14, -0.25, -0.005, -0.005, 0.0};
     double newK[9];
