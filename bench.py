@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--pool", type=int, default=0, help="distinct frames rendered per rank (default 2*batch+1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP-event timing")
+    ap.add_argument("--host-trace", action="store_true", help="print host-side enqueue times per step to stderr")
     ap.add_argument("--dropin-seconds", type=float, default=4.0,
                     help="bounded timing of the per-pair drop-in surface (0 = skip)")
     ap.add_argument("--streams", type=int, default=2,
@@ -132,12 +133,18 @@ def main():
     torch.cuda.synchronize()
     n_windows = max(1, (pool_n - 1) // B)
 
+    host_log = []
+
     def step(i):
         s = (i % n_windows) * B
         k = i % S
         fs = fss[k]
+        t_a = time.perf_counter()
         fs.process(pool[s:s + B + 1], recs_t[k], wait_torch=False)
+        t_b = time.perf_counter()
         fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
+        if args.host_trace:
+            host_log.append((i, t_a, t_b, time.perf_counter()))
 
     def sync_all():
         for f in fss:
@@ -156,6 +163,9 @@ def main():
         step(args.warmup + i)
     sync_all()
     elapsed = time.perf_counter() - t0
+    for i, t_a, t_b, t_c in host_log:
+        print(f"host step {i}: process enqueued at {1e3 * (t_a - t0):8.2f} ms, took {1e3 * (t_b - t_a):6.2f} ms; "
+              f"pose_tail {1e3 * (t_c - t_b):6.2f} ms", file=sys.stderr)
 
     recs = FrameStream.records_numpy(recs_t[(args.warmup + args.steps - 1) % S], B)
     stage_ms, calls = {}, 0

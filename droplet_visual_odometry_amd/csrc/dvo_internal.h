@@ -14,8 +14,30 @@
 
 namespace dvo {
 
+// Measurement-only experiment builds (tools/ab_dup.sh, never the product):
+// DVO_EXP_DUP is a bit mask of idempotent kernels launched twice, so the
+// default two-stream bench shows each one's marginal cost with the workload
+// unchanged.  0 in the product build.
+#ifndef DVO_EXP_DUP
+#define DVO_EXP_DUP 0
+#endif
+enum : int { kDupResize = 1, kDupBlur = 2, kDupFast = 4, kDupHarris = 8, kDupDescribe = 16, kDupMatch = 32,
+             kDupScore = 64, kDupSelect = 128 };
+#define DVO_LAUNCH(bit, ...)                            \
+    do {                                                \
+        hipLaunchKernelGGL(__VA_ARGS__);                \
+        if (DVO_EXP_DUP & (bit)) hipLaunchKernelGGL(__VA_ARGS__); \
+    } while (0)
+
 constexpr int kMaxLevels = 8;
-constexpr int kBandRows = 16;       // FAST tile height (output rows)
+// FAST tile height (output rows).  Two-stream bench, 1280x720: 16 rows 66.8-67.2 K
+// frames/s, 20: 67.7 K, 24: 68.2-69.1 K, 28: 65.7-66.1 K, 32: 67.1-67.9 K
+// (taller tiles: fewer barriers and carried rows per output row, more LDS per
+// workgroup; 24 rows = 6 workgroups per CU).
+#ifndef DVO_BAND_ROWS
+#define DVO_BAND_ROWS 24
+#endif
+constexpr int kBandRows = DVO_BAND_ROWS;
 constexpr int kFastTW = 126;        // FAST tile width (output columns; score window 128)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
@@ -79,7 +101,13 @@ struct RansacState {
     int32_t best_h, best_i;  // best model: hypothesis, root
     int32_t pad[2];
 };
-constexpr int kRansacRound1 = 64;   // hypotheses per pair in round 1
+// RANSAC rounds: round r solves hypotheses [bound[r-1], min(bound[r], niters)).
+#ifndef DVO_RANSAC_BOUNDS
+#define DVO_RANSAC_BOUNDS 64, 1 << 30
+#endif
+constexpr int kRansacBounds[] = {DVO_RANSAC_BOUNDS};
+constexpr int kRansacRounds = sizeof(kRansacBounds) / sizeof(int);
+constexpr int kRansacRound1 = kRansacBounds[0];  // hypotheses per pair in round 1
 
 struct Buffers {
     uint8_t* pyr;

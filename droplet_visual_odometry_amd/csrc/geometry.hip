@@ -974,8 +974,8 @@ __global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
 // them in parallel (one thread per hypothesis), counts inliers of every root
 // in parallel (one wave per model), then replays the sequential bookkeeping in
 // order (one thread per pair).  niters never grows, so round 1 covers
-// [0, min(256, niters)) and round 2 everything left, [256, niters): the result
-// is the sequential loop's, bit for bit.
+// [0, min(64, niters)) and round 2 everything left, [64, niters)
+// (kRansacBounds): the result is the sequential loop's, bit for bit.
 constexpr int kSolveNT = 64;
 #ifndef DVO_SCORE_CHUNK
 #define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
         }
     } else {
         h0 = S.h1;
-        h1 = (S.m > 5 && S.iter < S.niters) ? S.niters : h0;
+        h1 = (S.m > 5 && S.iter < S.niters) ? min(S.niters, kRansacBounds[round]) : h0;
     }
     const unsigned m = (unsigned)S.m;
     // x % m by Lemire's fastmod (exact for every 32-bit x and m)
@@ -1479,8 +1479,9 @@ __global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
 
 hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
     const int cap = g.hyp_cap;
-    for (int round = 0; round < 2; ++round) {
-        const int span = round == 0 ? min(kRansacRound1, cap) : cap - kRansacRound1;
+    for (int round = 0; round < kRansacRounds; ++round) {
+        const int lo = round == 0 ? 0 : kRansacBounds[round - 1];
+        const int span = min(kRansacBounds[round], cap) - lo;
         if (span <= 0) break;
         hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, pairs, round);
         const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
@@ -1491,7 +1492,7 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
         hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
         hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
         hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
+        DVO_LAUNCH(kDupScore, ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
                            s, g);
         hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
     }
@@ -1800,26 +1801,16 @@ __global__ void pose_tail_kernel(TailArgs a) {
 }
 
 // Prefix product T_abs[p] = T_abs[p-1] . T_rel[p], in pair order, and the
-// carry-out of P_prev / T_abs for the next batch.  One wave: lane 4r+c holds
-// T[r][c]; each step is U[r][c] = T[r][0]*A[0][c] + ... + T[r][3]*A[3][c] with
-// the row broadcast by DPP quad_perm, the same left-to-right arithmetic as a
-// scalar 4x4 product (bit-identical, no reassociation across steps).  T_rel is
-// staged through LDS 32 pairs at a time, off the dependency chain.
-__device__ __forceinline__ double quad_bcast(double v, int k) {
-    const int ctrl = k | (k << 2) | (k << 4) | (k << 6);
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
-    switch (ctrl) {  // dpp control must be an immediate
-        case 0x00: lo = __builtin_amdgcn_mov_dpp(lo, 0x00, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x00, 0xF, 0xF, false); break;
-        case 0x55: lo = __builtin_amdgcn_mov_dpp(lo, 0x55, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0x55, 0xF, 0xF, false); break;
-        case 0xAA: lo = __builtin_amdgcn_mov_dpp(lo, 0xAA, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xAA, 0xF, 0xF, false); break;
-        default: lo = __builtin_amdgcn_mov_dpp(lo, 0xFF, 0xF, 0xF, false); hi = __builtin_amdgcn_mov_dpp(hi, 0xFF, 0xF, 0xF, false); break;
-    }
-    return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
+// carry-out of P_prev / T_abs for the next batch.  The product is not
+// associative in floating point, so the chain stays sequential (bit-identical
+// to the scalar left-to-right 4x4 product); what is parallel is inside a step.
+// Row r of the running pose depends only on row r of the previous one, so
+// lane r (mod 4) keeps its whole row in registers and a step is 16 muls and
+// 12 adds in 4 independent column chains: no cross-lane traffic on the
+// dependency chain.  T_rel is staged through LDS 64 pairs at a time and read
+// one step ahead as wave-uniform broadcasts.
 __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
-    constexpr int kChunk = 32;
+    constexpr int kChunk = 64;
     __shared__ double tr[kChunk * 16];
     const int lane = threadIdx.x;
     int last_ok = -1;
@@ -1831,21 +1822,48 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
     }
-    const int c = lane & 3;
-    double t = a.tcarry[lane & 15];
+    const int r = lane & 3;
+    double t0 = a.tcarry[r * 4 + 0], t1 = a.tcarry[r * 4 + 1], t2 = a.tcarry[r * 4 + 2], t3 = a.tcarry[r * 4 + 3];
     for (int p0 = 0; p0 < a.pairs; p0 += kChunk) {
         const int n = min(kChunk, a.pairs - p0);
         __syncthreads();
         for (int i = lane; i < n * 16; i += 64) tr[i] = a.T_rel[(int64_t)p0 * 16 + i];
         __syncthreads();
+        // software pipeline: step q+1's T_rel is read from LDS while step q computes, so
+        // no LDS latency sits on the dependency chain
+        double A[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A[k] = tr[k];
         for (int q = 0; q < n; ++q) {
-            const double* A = tr + q * 16;
-            const double a0 = A[0 * 4 + c], a1 = A[1 * 4 + c], a2 = A[2 * 4 + c], a3 = A[3 * 4 + c];
-            t = quad_bcast(t, 0) * a0 + quad_bcast(t, 1) * a1 + quad_bcast(t, 2) * a2 + quad_bcast(t, 3) * a3;
-            if (lane < 16) a.T_abs[(int64_t)(p0 + q) * 16 + lane] = t;
+            const int qn = min(q + 1, n - 1);
+            double B[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) B[k] = tr[qn * 16 + k];  // the same address in every lane
+            const double u0 = t0 * A[0] + t1 * A[4] + t2 * A[8] + t3 * A[12];
+            const double u1 = t0 * A[1] + t1 * A[5] + t2 * A[9] + t3 * A[13];
+            const double u2 = t0 * A[2] + t1 * A[6] + t2 * A[10] + t3 * A[14];
+            const double u3 = t0 * A[3] + t1 * A[7] + t2 * A[11] + t3 * A[15];
+            t0 = u0;
+            t1 = u1;
+            t2 = u2;
+            t3 = u3;
+            if (lane < 4) {
+                double* o = a.T_abs + (int64_t)(p0 + q) * 16 + r * 4;
+                o[0] = t0;
+                o[1] = t1;
+                o[2] = t2;
+                o[3] = t3;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) A[k] = B[k];
         }
     }
-    if (lane < 16) a.tcarry[lane] = t;
+    if (lane < 4) {
+        a.tcarry[r * 4 + 0] = t0;
+        a.tcarry[r * 4 + 1] = t1;
+        a.tcarry[r * 4 + 2] = t2;
+        a.tcarry[r * 4 + 3] = t3;
+    }
     if (lane == 0 && last_ok >= 0 && a.carry) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
 }
 

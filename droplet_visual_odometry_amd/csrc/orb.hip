@@ -479,13 +479,13 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 
 // FAST over one column strip of one level.  The workgroup walks the strip's
 // tiles (kBandRows output rows x kFastTW (126) output columns) top to bottom.
-// The image window of a tile (rows [r0-4, r0+20), 144 columns from the aligned
-// column bx) lives in LDS as words; the next tile's 16 new rows are loaded into
+// The image window of a tile (rows [r0-4, r0+kBandRows+4), 144 columns from the
+// aligned column bx) lives in LDS as words; the next tile's kBandRows new rows are loaded into
 // registers while the current tile is processed (the load latency hides behind
 // the compute), and its last 8 rows are carried to the top of the window, so
 // every image byte is fetched from HBM once.  FAST scores are needed on the
 // NMS neighbourhood, score rows [r0-1, r1] x score columns [xs-1, xs+127): the
-// first tile computes all 18 score rows, later tiles the 16 new ones and carry
+// first tile computes all kBandRows+2 score rows, later tiles the kBandRows new ones and carry
 // the two above (and the corners of the last one, an output row of the next
 // tile, in a small list).  Per tile, phases separated by workgroup barriers;
 // the candidate lists are per-wave LDS segments that the next phase reads as
@@ -500,12 +500,12 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //   output   keeps per tile row in column order, (offset << 16 | count) per
 //            row; select_fast_kernel restores raster order across tiles.
 constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
-constexpr int kFtRows = kBandRows + 8;          // staged image rows per tile: [r0-4, r0+20)
+constexpr int kFtRows = kBandRows + 8;          // staged image rows per tile: [r0-4, r0+kBandRows+4)
 constexpr int kFtSeg = ((kBandRows + 2 + 3) / 4) * 128;  // per-wave list capacity (score rows sr == wid mod 4)
 constexpr int kFtWords = kFtLW / 4;             // words per staged row
-constexpr int kFtNewW = kBandRows * kFtWords;   // words loaded per tile (rows r0+4 .. r0+20)
+constexpr int kFtNewW = kBandRows * kFtWords;   // words loaded per tile (rows r0+4 .. r0+kBandRows+4)
 constexpr int kFtPf = (kFtNewW + kFastNT - 1) / kFastNT;
-constexpr int kFtCarryW = 8 * kFtWords;         // image words carried (rows r0+12 .. r0+20 -> top)
+constexpr int kFtCarryW = 8 * kFtWords;         // image words carried (the window's last 8 rows -> top)
 constexpr int kFtCarryR = (kFtCarryW + kFastNT - 1) / kFastNT;
 constexpr int kFtCarryList = 128;               // corners of one score row
 static_assert(kFtRows * kFtWords == kFtNewW + kFtCarryW, "staging covers the window");
@@ -540,8 +540,8 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
-    __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+20)
-    __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+17)
+    __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+kBandRows+4)
+    __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+kBandRows+1)
     // + 64 slots per wave that lanes without an entry store to (branch-free appends: no exec-mask SALU)
     __shared__ uint16_t cand[4 * kFtSeg + 256], corner[4 * kFtSeg + 256];
     __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
     // load returns whatever lies there (or 0 past the level).
     uint32_t creg[kFtCarryR], pf[kFtPf], screg = 0;
-    {  // prologue: rows [r0-4, r0+4) into the carry registers, [r0+4, r0+20) into the prefetch registers
+    {  // prologue: rows [r0-4, r0+4) into the carry registers, [r0+4, r0+kBandRows+4) into the prefetch registers
         const int ylo = kBorder - 4;
 #pragma unroll
         for (int k = 0; k < kFtCarryR; ++k) {
@@ -590,8 +590,8 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             if (q < kFtNewW) reinterpret_cast<uint32_t*>(img)[kFtCarryW + q] = pf[k];
         }
         if (threadIdx.x < 2 * kFtWords) reinterpret_cast<uint32_t*>(sc)[threadIdx.x] = b == 0 ? 0u : screg;
-        if (threadIdx.x < kBandRows * kFtLW / 16)
-            reinterpret_cast<uint4*>(sc + 2 * kFtLW)[threadIdx.x] = make_uint4(0, 0, 0, 0);
+        for (int q = threadIdx.x; q < kBandRows * kFtLW / 16; q += kFastNT)
+            reinterpret_cast<uint4*>(sc + 2 * kFtLW)[q] = make_uint4(0, 0, 0, 0);
         if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
         if (threadIdx.x == 0) ncarry[par ^ 1] = 0;
         __syncthreads();
@@ -694,10 +694,10 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             sc[a - 3 * kFtLW] = (uint8_t)fast_score16(cc, p[0], thr);
         }
         __syncthreads();
-        // score rows 16, 17 for the next tile (final now)
+        // score rows kBandRows, kBandRows+1 for the next tile (final now)
         if (threadIdx.x < 2 * kFtWords) screg = reinterpret_cast<const uint32_t*>(sc)[kBandRows * kFtWords + threadIdx.x];
         // ---- strict 3x3 NMS of the carried and new corners; keeps lie in rows [r0, r1), columns [xs, xe).
-        // New corners of score row 17 (row r0 + 16) are the next tile's row-1 corners.
+        // New corners of score row kBandRows+1 (row r0 + kBandRows) are the next tile's row-1 corners.
         for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
             const int a = (e < nc ? (int)carry[par][e] : seg_at(corner, cnt2, e - nc)) - 3 * kFtLW;  // score-plane address
             const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
@@ -1369,7 +1369,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
         // 32 * 1.25 + 2 rows <= kRsRows
         const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
         if (lds)
-            hipLaunchKernelGGL(resize_level_lds_kernel,
+            DVO_LAUNCH(kDupResize, resize_level_lds_kernel,
                                dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) * xcd_frames(F)),
                                dim3(256), 0, s, P, l, (pl.L[l].w + 255) / 256);
         else  // level pairs whose rounded sizes differ by more than 1.25x: tiny frames (8x8: levels 4->5, 6->7)
@@ -1378,20 +1378,20 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
-    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
+    DVO_LAUNCH(kDupBlur, blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
     if (pl.total_strips > 0)
-        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
+        DVO_LAUNCH(kDupFast, fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
-    hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
-    hipLaunchKernelGGL(harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
+    DVO_LAUNCH(kDupSelect, select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    DVO_LAUNCH(kDupHarris, harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
     hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
-    hipLaunchKernelGGL(describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
+    DVO_LAUNCH(kDupDescribe, describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
     mark(ev, 4, 1, s);
     return hipGetLastError();
 }

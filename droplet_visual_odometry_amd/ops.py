@@ -246,12 +246,22 @@ class Undistorter:
         self.ctx.check(self.ctx.lib.dvo_undistort_image(self.h_, ptr(img), img.strides[0], ptr(out), out.strides[0]))
         return out
 
-    def apply(self, src, dst, hip_stream=0):
-        """Remap n device frames (uint8 torch tensors [n, H, W], rows contiguous)."""
+    def apply(self, src, dst, hip_stream=None):
+        """Remap n device frames (uint8 torch tensors [n, H, W], rows contiguous)
+        on `hip_stream` (a non-NULL hipStream_t handle), by default ordered
+        with torch's current stream."""
         n = src.shape[0]
-        self.ctx.check(self.ctx.lib.dvo_undistort_apply(self.h_, src.data_ptr(), n, src.stride(0), src.stride(1),
-                                                        dst.data_ptr(), dst.stride(0), dst.stride(1),
-                                                        ctypes.c_void_p(hip_stream) if hip_stream else None))
+
+        def call(st):
+            self.ctx.check(self.ctx.lib.dvo_undistort_apply(self.h_, src.data_ptr(), n, src.stride(0), src.stride(1),
+                                                            dst.data_ptr(), dst.stride(0), dst.stride(1),
+                                                            ctypes.c_void_p(st)))
+        if hip_stream:
+            call(hip_stream)
+        else:
+            from .stream import ordered_side_stream
+            with ordered_side_stream(src.device) as st:
+                call(st)
 
     def map(self):
         xy = np.zeros((self.h, self.w, 2), np.int16)

@@ -10,6 +10,7 @@ only containers for device memory; all compute is in libdvo_hip.so.
 from __future__ import annotations
 
 import collections
+import contextlib
 import ctypes
 
 import numpy as np
@@ -188,11 +189,30 @@ class FrameStream:
             pass
 
 
+_side_streams = {}
+
+
+@contextlib.contextmanager
+def ordered_side_stream(device):
+    """A HIP stream handle for a library call that must behave as if it ran on
+    torch's current stream.  The C API reads a NULL stream as "the context's
+    stream" (non-blocking, unordered with torch's default stream), so calls
+    are made on a per-device side stream that waits for torch's current stream
+    before the call, and that torch's current stream waits for after it."""
+    cur = torch.cuda.current_stream(device)
+    side = _side_streams.get(device)
+    if side is None:
+        side = _side_streams[device] = torch.cuda.Stream(device)
+    side.wait_stream(cur)
+    yield side.cuda_stream
+    cur.wait_stream(side)
+
+
 class PoseChain:
     """Absolute-pose chain T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) on the
     device (dvo_pose_chain) with a persistent carry: the reassembly step of a
     sharded pose stream (dist.ShardedPoseStream).  Runs on torch's current
-    stream, where the all-gather that produced T_rel ran."""
+    stream, where the all-gather that produced T_rel ran (ordered_side_stream)."""
 
     def __init__(self, ctx: Context | None = None, device: int | None = None, T0=None):
         self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
@@ -212,8 +232,8 @@ class PoseChain:
             T_abs = torch.empty((n, 4, 4), dtype=torch.float64, device=self.device)
         if T_abs.shape[0] < n or not T_abs.is_contiguous():
             raise ValueError("T_abs must be a contiguous float64 [>= n, 4, 4] device tensor")
-        st = torch.cuda.current_stream(self.device).cuda_stream
-        self.ctx.check(self.ctx.lib.dvo_pose_chain(self.ctx.h, T_rel.data_ptr(), n, self.carry.data_ptr(),
-                                                   T_abs.data_ptr(), st))
+        with ordered_side_stream(self.device) as st:
+            self.ctx.check(self.ctx.lib.dvo_pose_chain(self.ctx.h, T_rel.data_ptr(), n, self.carry.data_ptr(),
+                                                       T_abs.data_ptr(), st))
         return T_abs
 

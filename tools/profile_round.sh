@@ -26,4 +26,8 @@ timeout -s KILL 170 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_sq -name '*counter_collection.csv') "$out/${tag}_pmc_sq.csv" > /dev/null
 python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" > /dev/null
 python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512
+# stall breakdown (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES, MI355X_MICROARCH.md PMC slots)
+timeout -s KILL 170 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+  -d /tmp/pmc_${tag}_stall -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_stall.log" 2>&1 &&
+python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_stall -name '*counter_collection.csv') "$out/${tag}_pmc_stall.csv" > /dev/null || echo "stall pass failed"
 rm -rf /tmp/st_$tag /tmp/pmc_${tag}_* /tmp/cal_${tag}_*
