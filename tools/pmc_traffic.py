@@ -10,6 +10,7 @@ factor of the access width it uses (KERNEL_WIDTHS, from the kernel source);
 kernels not listed keep their raw readings (calibrated: false)."""
 import csv
 import json
+import os
 import sys
 
 # (read width, write width) of the dominant accesses, per kernel (orb.hip)
@@ -52,7 +53,7 @@ def main(fetch, write, sq, calib, dst, batch=1024):
         "unit": "per launch: bytes (FETCH_SIZE/WRITE_SIZE KB x1024, then the width calibration), "
                 "SQ_* instruction counts (wave-level)",
         "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts), mean over dispatches",
-        "calibration": calib,
+        "calibration": os.path.basename(calib),
         "kernels": kernels,
     }
     json.dump(doc, open(dst, "w"), indent=1)
