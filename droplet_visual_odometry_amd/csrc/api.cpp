@@ -28,11 +28,19 @@ struct SiftPlanDev {  // per-size device buffers of dvo_sift_detect_and_compute
     std::vector<void*> allocs;
 };
 
+struct SurfPlanDev {  // per-size device buffers of dvo_surf_detect_and_compute
+    int w = 0, h = 0;
+    SurfArgs a{};
+    uint8_t* img = nullptr;
+    std::vector<void*> allocs;
+};
+
 struct dvo_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
     SiftPlanDev sift;
+    SurfPlanDev surf;
     // grow-only scratch for the per-call entry points
     std::vector<std::pair<void*, size_t>> scratch;
     dvo_stream* call_stream = nullptr;  // cached plan for detectAndCompute
@@ -427,6 +435,7 @@ void dvo_ctx_destroy(dvo_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     for (void* p : ctx->sift.allocs) hipFree(p);
+    for (void* p : ctx->surf.allocs) hipFree(p);
     if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
     for (auto& e : ctx->scratch)
         if (e.first) hipFree(e.first);
@@ -845,6 +854,152 @@ int sift_plan(dvo_ctx* ctx, int w, int h) {
     return DVO_OK;
 }
 }  // namespace
+
+namespace {
+// getGaussianKernel(n, sigma, CV_32F) as oracle/surf.cpp restates it
+std::vector<float> surf_gauss(int n, double sigma) {
+    std::vector<float> k(n);
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; ++i) {
+        const double x = i - (n - 1) * 0.5;
+        k[i] = (float)std::exp(scale2X * x * x);
+        sum += k[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
+    return k;
+}
+
+// resizeHaarPattern (surf.cpp) on the host: offsets in an integral image of row step `step`
+void surf_haar(const int src[][5], SurfHaar* dst, int n, int old_size, int new_size, int step) {
+    const float ratio = (float)new_size / old_size;
+    for (int k = 0; k < n; ++k) {
+        const int dx1 = (int)std::nearbyint(ratio * src[k][0]), dy1 = (int)std::nearbyint(ratio * src[k][1]);
+        const int dx2 = (int)std::nearbyint(ratio * src[k][2]), dy2 = (int)std::nearbyint(ratio * src[k][3]);
+        dst[k].p0 = dy1 * step + dx1;
+        dst[k].p1 = dy2 * step + dx1;
+        dst[k].p2 = dy1 * step + dx2;
+        dst[k].p3 = dy2 * step + dx2;
+        dst[k].w = src[k][4] / ((float)(dx2 - dx1) * (dy2 - dy1));
+    }
+}
+
+int surf_plan(dvo_ctx* ctx, int w, int h) {
+    SurfPlanDev& P = ctx->surf;
+    if (P.w == w && P.h == h) return DVO_OK;
+    for (void* p : P.allocs) hipFree(p);
+    P = SurfPlanDev{};
+    SurfArgs& A = P.a;
+    A.w = w;
+    A.h = h;
+    A.pitch = (w + 255) & ~255;
+    const int sw = w + 1;
+    static const int dx_s[3][5] = {{0, 2, 3, 7, 1}, {3, 2, 6, 7, -2}, {6, 2, 9, 7, 1}};
+    static const int dy_s[3][5] = {{2, 0, 7, 3, 1}, {2, 3, 7, 6, -2}, {2, 6, 7, 9, 1}};
+    static const int dxy_s[4][5] = {{1, 1, 4, 4, 1}, {5, 1, 8, 4, -1}, {1, 5, 4, 8, -1}, {5, 5, 8, 8, 1}};
+    std::vector<SurfHaar> haar((size_t)kSurfTot * 10);
+    int64_t cells = 0;
+    for (int o = 0; o < kSurfOct; ++o) {
+        const int step = 1 << o;
+        A.rows[o] = h / step;
+        A.cols[o] = w / step;
+        for (int l = 0; l < kSurfLayers; ++l) {
+            const int L = o * kSurfLayers + l;
+            A.size[L] = (9 + 6 * l) << o;
+            A.off[L] = cells;
+            cells += (int64_t)A.rows[o] * A.cols[o];
+            surf_haar(dx_s, &haar[L * 10], 3, 9, A.size[L], sw);
+            surf_haar(dy_s, &haar[L * 10 + 3], 3, 9, A.size[L], sw);
+            surf_haar(dxy_s, &haar[L * 10 + 6], 4, 9, A.size[L], sw);
+        }
+    }
+    // SURF_ORI_SIGMA 2.5f, SURF_DESC_SIGMA 3.3f: float constants widened to double
+    const std::vector<float> go = surf_gauss(13, (double)2.5f), gd = surf_gauss(20, (double)3.3f);
+    std::vector<int8_t> apt;
+    std::vector<float> aptw;
+    for (int i = -6; i <= 6; ++i)
+        for (int j = -6; j <= 6; ++j)
+            if (i * i + j * j <= 36) {
+                apt.push_back((int8_t)i);
+                apt.push_back((int8_t)j);
+                aptw.push_back(go[i + 6] * go[j + 6]);
+            }
+    A.nori = (int)aptw.size();
+    for (int i = 0; i < 20; ++i) A.gdesc[i] = gd[i];
+    A.kp_cap = std::max(4096, (w * h) / 64);
+    int order_n = 1;
+    while (order_n < A.kp_cap) order_n <<= 1;
+    auto A_ = [&](auto*& p, size_t bytes) {
+        void* q = nullptr;
+        if (hipMalloc(&q, bytes ? bytes : 16) != hipSuccess) return false;
+        P.allocs.push_back(q);
+        p = static_cast<std::remove_reference_t<decltype(p)>>(q);
+        return true;
+    };
+    int* counters = nullptr;
+    SurfHaar* d_haar = nullptr;
+    int8_t* d_apt = nullptr;
+    float* d_aptw = nullptr;
+    if (!A_(A.sum, (size_t)sw * (h + 1) * 4) || !A_(A.det, (size_t)cells * 4) || !A_(A.trace, (size_t)cells * 4) ||
+        !A_(A.raw, (size_t)A.kp_cap * sizeof(dvo_keypoint)) || !A_(A.order, (size_t)order_n * 4) ||
+        !A_(A.kps, (size_t)A.kp_cap * sizeof(dvo_keypoint)) || !A_(A.dtmp, (size_t)A.kp_cap * 64 * 4) ||
+        !A_(A.out, (size_t)A.kp_cap * sizeof(dvo_keypoint)) || !A_(A.desc, (size_t)A.kp_cap * 64 * 4) ||
+        !A_(counters, 64) || !A_(d_haar, haar.size() * sizeof(SurfHaar)) || !A_(d_apt, apt.size()) ||
+        !A_(d_aptw, aptw.size() * 4) || !A_(P.img, (size_t)A.pitch * h)) {
+        for (void* p : P.allocs) hipFree(p);
+        P = SurfPlanDev{};
+        return fail(ctx, DVO_EHIP, "SURF buffers: hipMalloc failed");
+    }
+    A.nraw = counters;
+    A.nout = counters + 1;
+    A.flags = counters + 2;
+    A.haar = d_haar;
+    A.apt = d_apt;
+    A.aptw = d_aptw;
+    A.img = P.img;
+    if (hipMemcpy(d_haar, haar.data(), haar.size() * sizeof(SurfHaar), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_apt, apt.data(), apt.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_aptw, aptw.data(), aptw.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(ctx, DVO_EHIP, "SURF tables upload failed");
+    P.w = w;
+    P.h = h;
+    return DVO_OK;
+}
+}  // namespace
+
+int dvo_surf_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, double hessian_threshold,
+                                dvo_keypoint* kps, float* desc, int cap, int* n_out) {
+    if (!ctx || !n_out) return DVO_EINVAL;
+    *n_out = 0;
+    if (!img || stride < w) return fail(ctx, DVO_EINVAL, "bad image buffer");
+    if (w < 1 || h < 1 || w >= kMaxW || h >= kMaxW) return fail(ctx, DVO_EINVAL, "image size out of range (1..4095)");
+    if (!(hessian_threshold >= 0)) return fail(ctx, DVO_EINVAL, "hessianThreshold must be >= 0");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = surf_plan(ctx, w, h);
+    if (rc) return rc;
+    SurfPlanDev& P = ctx->surf;
+    P.a.thr = (float)hessian_threshold;
+    HIP_TRY(hipMemsetAsync(P.a.nraw, 0, 16, ctx->stream));
+    const int64_t cells = P.a.off[kSurfTot - 1] + (int64_t)P.a.rows[kSurfOct - 1] * P.a.cols[kSurfOct - 1];
+    HIP_TRY(hipMemsetAsync(P.a.det, 0, (size_t)cells * 4, ctx->stream));
+    HIP_TRY(hipMemsetAsync(P.a.trace, 0, (size_t)cells * 4, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(P.img, P.a.pitch, img, stride, w, h, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(launch_surf(P.a, ctx->stream));
+    int cnt[3];
+    HIP_TRY(hipMemcpyAsync(cnt, P.a.nraw, 12, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (cnt[2]) return fail(ctx, DVO_ECAP, "SURF: more keypoints than the device lists hold");
+    const int n = cnt[1];
+    *n_out = n;
+    if (n > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    if (n) {
+        if (kps) HIP_TRY(hipMemcpyAsync(kps, P.a.out, (size_t)n * sizeof(dvo_keypoint), hipMemcpyDeviceToHost, ctx->stream));
+        if (desc) HIP_TRY(hipMemcpyAsync(desc, P.a.desc, (size_t)n * 64 * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
+    return DVO_OK;
+}
 
 int dvo_sift_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, dvo_keypoint* kps,
                                 float* desc, int cap, int* n_out) {

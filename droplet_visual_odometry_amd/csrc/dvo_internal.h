@@ -241,6 +241,40 @@ struct SiftArgs {
     int* flags;             // 1: candidate overflow, 2: keypoint overflow
 };
 
+// SURF_create(hessianThreshold).detectAndCompute (surf.hip): nOctaves 4,
+// nOctaveLayers 3, 64-d descriptors, orientation on.
+constexpr int kSurfOct = 4, kSurfLayers = 5, kSurfTot = kSurfOct * kSurfLayers;
+struct SurfHaar {  // resizeHaarPattern output: 4 corner offsets + weight (host-built)
+    int p0, p1, p2, p3;
+    float w;
+};
+struct SurfArgs {
+    const uint8_t* img;     // device copy of the image (pitch)
+    int w, h, pitch;
+    int32_t* sum;           // integral image, (h + 1) x (w + 1)
+    float* det;             // per layer: rows x cols of the layer's octave
+    float* trace;
+    int64_t off[kSurfTot];  // element offset of each layer in det / trace
+    int size[kSurfTot];     // (9 + 6 layer) << octave
+    int rows[kSurfOct], cols[kSurfOct];
+    const SurfHaar* haar;   // [kSurfTot][10]: Dx (3), Dy (3), Dxy (4) of calcLayerDetAndTrace
+    const int8_t* apt;      // 113 x (i, j): the orientation disc, apt[n] = Point(i, j)
+    const float* aptw;      // 113 weights gori[i + 6] * gori[j + 6]
+    float thr;              // hessianThreshold
+    dvo_keypoint* raw;      // extrema after interpolation (unsorted)
+    int* nraw;
+    int kp_cap;
+    int32_t* order;         // sort scratch, next power of two >= kp_cap
+    dvo_keypoint* kps;      // sorted (KeypointGreater), then oriented; size -1 = dropped
+    float* dtmp;            // kp_cap x 64, descriptors in sorted order
+    dvo_keypoint* out;      // compacted keypoints
+    float* desc;            // compacted descriptors
+    int* nout;
+    int* flags;             // 2: keypoint overflow
+    int nori;               // samples in the orientation disc (113)
+    float gdesc[20];        // getGaussianKernel(20, 3.3)
+};
+
 // ---- host entry points of the kernels (implemented in the .hip files) -------
 // ev: optional table of 2*DVO_NSTAGES events recorded around each stage.
 inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
@@ -287,6 +321,7 @@ size_t match_pair_work_size(int nq, int nt);
 // d_taps: the 6 Gaussian kernels (initial blur, layers 1..5) back to back.
 hipError_t launch_sift(const SiftArgs& A, const uint8_t* d_img, int w, int h, int stride, const float* d_taps,
                        const int* tap_off, const int* tap_n, hipStream_t s);
+hipError_t launch_surf(const SurfArgs& a, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,

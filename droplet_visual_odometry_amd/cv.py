@@ -480,14 +480,6 @@ def drawKeypoints(image, keypoints, outImage=None, color=(0, 255, 0), flags=0):
     return out
 
 
-def _host_cv2():
-    try:
-        import cv2  # noqa: F401  (detection only; matching stays on the GPU)
-        return cv2
-    except ImportError:
-        return None
-
-
 class SIFT:
     """cv2.SIFT with SIFT_create()'s defaults (v3:100), on the GPU
     (dvo_sift_detect_and_compute): keypoints and float32[N, 128] descriptors
@@ -521,10 +513,47 @@ def SIFT_create(nfeatures=0, nOctaveLayers=3, contrastThreshold=0.04, edgeThresh
     return SIFT(nfeatures, nOctaveLayers, contrastThreshold, edgeThreshold, sigma)
 
 
+class SURF:
+    """cv2.xfeatures2d.SURF (v3:104, SURF_create(400)) on the GPU
+    (dvo_surf_detect_and_compute): keypoints and float32[N, 64] descriptors for
+    the surf mode's NORM_L1 knnMatch (v3:215)."""
+
+    def __init__(self, hessianThreshold=100, nOctaves=4, nOctaveLayers=3, extended=False, upright=False):
+        if nOctaves != 4 or nOctaveLayers != 3 or extended or upright:
+            raise error("only nOctaves 4, nOctaveLayers 3, extended False, upright False are implemented "
+                        "(the reference's SURF_create(400), v3:104)")
+        if not hessianThreshold >= 0:
+            raise error("hessianThreshold must be >= 0")
+        self.hessianThreshold = float(hessianThreshold)
+
+    def detectAndCompute(self, image, mask, descriptors=None, useProvidedKeypoints=False):
+        if mask is not None:
+            raise error("SURF masks are not supported (the reference passes None, v3:373)")
+        if useProvidedKeypoints:
+            raise error("useProvidedKeypoints is not supported")
+        img = _gray(image)
+        try:
+            kps, desc = ops.surf_detect_and_compute(img, self.hessianThreshold)
+        except DVOError as e:
+            raise error(str(e)) from e
+        return KeyPoints(kps), (desc if len(kps) else None)
+
+    def detect(self, image, mask=None):
+        return self.detectAndCompute(image, mask)[0]
+
+    def descriptorSize(self):
+        return 64
+
+    def getHessianThreshold(self):
+        return self.hessianThreshold
+
+
+def SURF_create(hessianThreshold=100, nOctaves=4, nOctaveLayers=3, extended=False, upright=False):
+    return SURF(hessianThreshold, nOctaves, nOctaveLayers, extended, upright)
+
+
 class _XFeatures2d:
-    """cv2.xfeatures2d: SIFT on the GPU (v3:100); SURF (v3:104, patented,
-    contrib-only) is not implemented on the device and comes from a host cv2
-    contrib build when one is importable, else cv.error."""
+    """cv2.xfeatures2d: SIFT (v3:100) and SURF (v3:104) on the GPU."""
 
     @staticmethod
     def SIFT_create(*a, **k):
@@ -532,10 +561,7 @@ class _XFeatures2d:
 
     @staticmethod
     def SURF_create(*a, **k):
-        cv2 = _host_cv2()
-        if cv2 is None or not hasattr(cv2, "xfeatures2d"):
-            raise error("SURF detection needs the host cv2 contrib package (not installed); matching is on the GPU")
-        return cv2.xfeatures2d.SURF_create(*a, **k)
+        return SURF_create(*a, **k)
 
 
 xfeatures2d = _XFeatures2d()

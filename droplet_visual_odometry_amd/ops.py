@@ -72,6 +72,29 @@ def sift_detect_and_compute(img: np.ndarray, ctx=None):
         return kps[:n.value].copy(), desc[:n.value].copy()
 
 
+def surf_detect_and_compute(img: np.ndarray, hessian_threshold: float = 400.0, ctx=None):
+    """xfeatures2d.SURF_create(hessian_threshold).detectAndCompute(img, None) on
+    the GPU (dvo_surf_detect_and_compute): KEYPOINT_DTYPE array (OpenCV's
+    KeypointGreater order) and float32[N, 64] descriptors."""
+    c = _ctx(ctx)
+    img = np.ascontiguousarray(img)
+    if img.dtype != np.uint8 or img.ndim != 2:
+        raise DVOError(-1, "surf_detect_and_compute expects a mono8 image (uint8[H, W])")
+    h, w = img.shape
+    cap = 8192
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 64), np.float32)
+        n = ctypes.c_int()
+        rc = c.lib.dvo_surf_detect_and_compute(c.h, ptr(img), w, h, img.strides[0], float(hessian_threshold), ptr(kps),
+                                               ptr(desc), cap, ctypes.byref(n))
+        if rc == DVO_ECAP and n.value > cap:
+            cap = n.value
+            continue
+        c.check(rc)
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+
 def bf_match(dq: np.ndarray, dt: np.ndarray, cross_check: int = 1, ctx=None) -> np.ndarray:
     """DMATCH_DTYPE array in queryIdx order (OpenCV's output order)."""
     c = _ctx(ctx)

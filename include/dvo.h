@@ -102,6 +102,17 @@ int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int
 int dvo_sift_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, dvo_keypoint* kps,
                                 float* desc, int cap, int* n_out);
 
+/* Replaces cv::xfeatures2d::SURF_create(hessianThreshold).detectAndCompute(img,
+ * None) — the detector of the 'surf' mode, visual_odometry_v3.py:104
+ * (SURF_create(400)) and :373 (call).  Other parameters at their defaults
+ * (nOctaves 4, nOctaveLayers 3, extended false, upright false).  img: host
+ * mono8.  kps: keypoints in OpenCV's KeypointGreater order (response, size,
+ * octave descending, then y descending, x ascending), class_id = sign of the
+ * Hessian trace; desc: n x 64 floats, unit norm.  *n_out = count (DVO_ECAP if
+ * > cap). */
+int dvo_surf_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, int stride, double hessian_threshold,
+                                dvo_keypoint* kps, float* desc, int cap, int* n_out);
+
 /* Replaces cv::findEssentialMat(points1, points2, K, RANSAC, prob, threshold,
  * maxIters) — visual_odometry_v3.py:297-300.  p1/p2: m x 2 doubles (pixel
  * coords, the float32 KeyPoint_convert output widened).  E receives 3 rows

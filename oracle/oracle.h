@@ -88,6 +88,12 @@ int ora_ransac_replay(const int32_t* nmod, const int32_t* cnt, int n, int m, dou
 int ora_sift_detect_and_compute(const uint8_t* img, int w, int h, int stride, ora_keypoint* kps, float* desc, int cap,
                                 int* n_out);
 
+// ---- SURF_create(hessian).detectAndCompute (surf.cpp; the 'surf' mode,
+// visual_odometry_v3.py:103-106, :373): nOctaves 4, nOctaveLayers 3, 64-d.
+// kps in KeypointGreater order; desc: n x 64 floats.  -5 when cap < n.
+int ora_surf_detect_and_compute(const uint8_t* img, int w, int h, int stride, double hessian_threshold,
+                                ora_keypoint* kps, float* desc, int cap, int* n_out);
+
 /* Image pre-processing (undistort.cpp): cv::getOptimalNewCameraMatrix and
  * cv::undistort (striped initUndistortRectifyMap + remap INTER_LINEAR,
  * BORDER_CONSTANT).  xy / frac receive the 16SC2 / 16UC1 maps (w*h). */

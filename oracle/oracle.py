@@ -92,6 +92,7 @@ def lib():
             "ora_ransac_subsets": [_c, _c, _i32p],
             "ora_ransac_replay": [_i32p, _i32p, _c, _c, _d, _c, _i32p],
             "ora_sift_detect_and_compute": [_u8p, _c, _c, _c, _kpp, _f32p, _c, _ip],
+            "ora_surf_detect_and_compute": [_u8p, _c, _c, _c, ctypes.c_double, _kpp, _f32p, _c, _ip],
             "ora_get_optimal_new_camera_matrix": [_f64p, _f64p, _c, _c, _c, _d, _c, _c, _f64p],
             "ora_undistort": [_u8p, _c, _c, _c, _f64p, _f64p, _c, ctypes.c_void_p, _u8p, _c,
                               np.ctypeslib.ndpointer(np.int16, flags="C"), np.ctypeslib.ndpointer(np.uint16, flags="C")],
@@ -175,6 +176,24 @@ def sift_detect_and_compute(img):
         if rc == -5:
             cap = n.value
             continue
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def surf_detect_and_compute(img, hessian_threshold=400.0):
+    """xfeatures2d.SURF_create(hessian_threshold).detectAndCompute(img, None):
+    (KEYPOINT_DTYPE array, float32[n, 64])."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = 4096
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 64), np.float32)
+        n = ctypes.c_int()
+        rc = lib().ora_surf_detect_and_compute(img, w, h, w, float(hessian_threshold), kps, desc, cap, ctypes.byref(n))
+        if rc == -5:
+            cap = n.value
+            continue
+        assert rc == 0, rc
         return kps[:n.value].copy(), desc[:n.value].copy()
 
 

@@ -130,6 +130,17 @@ int main() {
         ora_ransac_replay(nmod.data(), cnt.data(), 0, 200, 0.999, 1000, out.data());
     }
 
+    // SURF, textured, a cap below the count and a tiny frame
+    {
+        std::vector<ora_keypoint> uk(8192);
+        std::vector<float> ud(8192 * 64);
+        int nu = 0;
+        EXPECT(ora_surf_detect_and_compute(a.data(), W, H, W, 400.0, uk.data(), ud.data(), 8192, &nu) == 0 && nu > 0);
+        ora_surf_detect_and_compute(a.data(), W, H, W, 400.0, uk.data(), ud.data(), 2, &nu);
+        std::vector<uint8_t> tiny((size_t)12 * 9, 200);
+        ora_surf_detect_and_compute(tiny.data(), 12, 9, 12, 0.0, uk.data(), ud.data(), 8192, &nu);
+    }
+
     // SIFT, textured and blank
     {
         std::vector<ora_keypoint> sk(4000);

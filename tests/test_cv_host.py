@@ -42,6 +42,10 @@ def test_unsupported_modes_raise_cv_error():
     with pytest.raises(cv.error):
         cv.xfeatures2d.SIFT_create(nOctaveLayers=4)  # only SIFT_create()'s defaults (v3:100)
     with pytest.raises(cv.error):
+        cv.xfeatures2d.SURF_create(400, extended=True)  # only SURF_create(400)'s other defaults (v3:104)
+    with pytest.raises(cv.error):
+        cv.xfeatures2d.SURF_create(400).detectAndCompute(np.zeros((8, 8), np.uint8), np.ones((8, 8), np.uint8))
+    with pytest.raises(cv.error):
         cv.SIFT_create().detectAndCompute(np.zeros((8, 8), np.uint8), np.ones((8, 8), np.uint8))
     with pytest.raises(cv.error):
         cv.BFMatcher(cv.NORM_HAMMING, True).knnMatch(None, None, k=2)

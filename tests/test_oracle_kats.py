@@ -264,3 +264,23 @@ def test_oracle_subsets_follow_cv_rng(oracle_mod):
         return out
     for m, n in [(6, 50), (9, 200), (871, 300)]:
         assert oracle_mod.ransac_subsets(m, n).tolist() == ref(m, n)
+
+
+def test_surf_restatement_invariants(oracle_mod):
+    """oracle/surf.cpp (SURF_create(400), the 'surf' mode, v3:104): keypoints in
+    KeypointGreater order, sizes integral after interpolation, class_id the
+    sign of the Hessian trace, unit-norm 64-d descriptors, orientation in
+    [0, 360), octaves 0..3.  (OpenCV's own output is not available here:
+    parity against it is unpinned.)"""
+    from conftest import synth_frames
+    frames, _ = synth_frames(320, 240, range(1))
+    k, d = oracle_mod.surf_detect_and_compute(frames[0], 400.0)
+    assert len(k) > 100 and d.shape == (len(k), 64)
+    np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=1e-5)
+    assert np.all(np.diff(k["response"]) <= 0)
+    assert np.all(k["size"] == np.round(k["size"])) and np.all(k["size"] >= 9 - 6)
+    assert set(np.unique(k["class_id"])) <= {-1, 1}
+    assert np.all((k["angle"] >= 0) & (k["angle"] < 360))
+    assert set(np.unique(k["octave"])) <= {0, 1, 2, 3}
+    k2, d2 = oracle_mod.surf_detect_and_compute(frames[0], 800.0)
+    assert len(k2) < len(k) and np.all(k2["response"] > 800)
