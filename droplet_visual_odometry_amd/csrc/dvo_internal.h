@@ -14,20 +14,6 @@
 
 namespace dvo {
 
-// Measurement-only experiment builds (tools/ab_dup.sh, never the product):
-// DVO_EXP_DUP is a bit mask of idempotent kernels launched twice, so the
-// default two-stream bench shows each one's marginal cost with the workload
-// unchanged.  0 in the product build.
-#ifndef DVO_EXP_DUP
-#define DVO_EXP_DUP 0
-#endif
-enum : int { kDupResize = 1, kDupBlur = 2, kDupFast = 4, kDupHarris = 8, kDupDescribe = 16, kDupMatch = 32,
-             kDupScore = 64, kDupSelect = 128 };
-#define DVO_LAUNCH(bit, ...)                            \
-    do {                                                \
-        hipLaunchKernelGGL(__VA_ARGS__);                \
-        if (DVO_EXP_DUP & (bit)) hipLaunchKernelGGL(__VA_ARGS__); \
-    } while (0)
 
 constexpr int kMaxLevels = 8;
 // FAST tile height (output rows).  Two-stream bench, 1280x720: 16 rows 66.8-67.2 K

@@ -991,7 +991,7 @@ constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 // duplicate; the first such lane redoes its subset with the rejection loop
 // (wave-uniform, ~1% of subsets) and the next 64 start after it.
 constexpr int kSampleBuf = 1024;  // MWC states staged per refill
-__global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round) {
+__global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round, int bound) {
     const int p = blockIdx.x;
     if (p >= pairs) return;
     const int lane = threadIdx.x;
@@ -1013,7 +1013,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
             if (lane < 5) idx[lane] = lane;
             h1 = 1;
         } else {
-            h1 = min(kRansacRound1, S.niters);
+            h1 = min(bound, S.niters);
         }
         if (S.m <= 5) {
             S.h0 = h0;
@@ -1023,7 +1023,7 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
         }
     } else {
         h0 = S.h1;
-        h1 = (S.m > 5 && S.iter < S.niters) ? min(S.niters, kRansacBounds[round]) : h0;
+        h1 = (S.m > 5 && S.iter < S.niters) ? min(S.niters, bound) : h0;
     }
     const unsigned m = (unsigned)S.m;
     // x % m by Lemire's fastmod (exact for every 32-bit x and m)
@@ -1477,13 +1477,21 @@ __global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
     }
 }
 
+// A few pairs leave the GPU idle, so they take one round over every hypothesis
+// up to maxIters: one Durand-Kerner tail instead of two (the per-call
+// findEssentialMat of the drop-in surface: 2.3 -> ~1.2 ms).  Rounds only
+// schedule the same hypotheses; the replay's result is the same.
+constexpr int kOneRoundPairs = 4;
 hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
     const int cap = g.hyp_cap;
-    for (int round = 0; round < kRansacRounds; ++round) {
+    const bool one = pairs <= kOneRoundPairs;
+    const int rounds = one ? 1 : kRansacRounds;
+    for (int round = 0; round < rounds; ++round) {
+        const int hi = one ? cap : kRansacBounds[round];
         const int lo = round == 0 ? 0 : kRansacBounds[round - 1];
-        const int span = min(kRansacBounds[round], cap) - lo;
+        const int span = min(hi, cap) - lo;
         if (span <= 0) break;
-        hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, pairs, round);
+        hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, pairs, round, hi);
         const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
         hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
         hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
@@ -1492,7 +1500,7 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
         hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
         hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
         hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        DVO_LAUNCH(kDupScore, ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
+        hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
                            s, g);
         hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
     }
@@ -1957,7 +1965,7 @@ hipError_t launch_pose_chain(const double* T_rel, int n, double* T_carry, double
 // Test hooks: the sampler / replay kernels on one pair whose RansacState the
 // caller set (api.cpp dvo_test_ransac_*).
 hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s) {
-    hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, s, g, 1, 1);
+    hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, s, g, 1, 1, 1 << 30);
     return hipGetLastError();
 }
 hipError_t launch_test_ransac_replay(const GeomArgs& g, hipStream_t s) {

@@ -346,7 +346,7 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     if (e != hipSuccess) return e;
     const int pairs = P.nframes - 1, nqb = (cap + kMQB - 1) / kMQB;
     const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
-    DVO_LAUNCH(kDupMatch, nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb, 1);
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb, 1);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();

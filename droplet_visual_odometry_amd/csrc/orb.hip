@@ -1369,7 +1369,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
         // 32 * 1.25 + 2 rows <= kRsRows
         const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
         if (lds)
-            DVO_LAUNCH(kDupResize, resize_level_lds_kernel,
+            hipLaunchKernelGGL(resize_level_lds_kernel,
                                dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) * xcd_frames(F)),
                                dim3(256), 0, s, P, l, (pl.L[l].w + 255) / 256);
         else  // level pairs whose rounded sizes differ by more than 1.25x: tiny frames (8x8: levels 4->5, 6->7)
@@ -1378,20 +1378,20 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
-    DVO_LAUNCH(kDupBlur, blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
     if (pl.total_strips > 0)
-        DVO_LAUNCH(kDupFast, fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
+        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
-    DVO_LAUNCH(kDupSelect, select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
-    DVO_LAUNCH(kDupHarris, harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    hipLaunchKernelGGL(harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
     hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
-    DVO_LAUNCH(kDupDescribe, describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
     mark(ev, 4, 1, s);
     return hipGetLastError();
 }
