@@ -1090,7 +1090,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.E = (double*)dE;
     g.info = (int32_t*)dinfo;
     g.mask = (uint8_t*)dmask;
-    HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStageRansac, ctx->stream));
+    HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStageRansac | kStageOneRound, ctx->stream));
     int info[4];
     HIP_TRY(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

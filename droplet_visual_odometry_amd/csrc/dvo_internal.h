@@ -200,6 +200,11 @@ struct GeomArgs {
 };
 
 constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;
+// kStageOneRound: the per-call findEssentialMat (one pair): a single RANSAC round
+// over every hypothesis up to maxIters, solved with one lane per root.  Stream
+// batches keep the two-round schedule, so their records (n_hypotheses) do not
+// depend on how a stream is split into batches or shards.
+constexpr int kStageOneRound = 8;
 
 // SIFT_create().detectAndCompute of one image (sift.hip).  Octave o has
 // size ow[o] x oh[o] (octave 0 = the 2x upscaled input); its Gaussian layer l

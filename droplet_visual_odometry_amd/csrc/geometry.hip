@@ -1235,6 +1235,122 @@ void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
     }
 }
 
+// Durand-Kerner with one lane per root, for rounds with few polynomials (the
+// per-call findEssentialMat of the drop-in surface: at most a few thousand
+// polynomials, so the one-lane kernel's ~1,750-instruction sweep on a single
+// wave per SIMD is the whole latency).  A 16-lane row holds one polynomial,
+// lane r < 10 owns root r and keeps a copy of all ten.  A sweep is the same
+// Gauss-Seidel order as dk_sweep: every lane forms its numerator (Horner at its
+// still-old root) at once; then for t = 0..9 lane t completes its denominator
+// with the old roots t+1..9, divides and updates, the new root t is broadcast
+// to the row (DPP row_newbcast), and the lanes r > t multiply in their factor
+// (z_r - z_t new) -- each lane's product is the reference's left-to-right chain
+// over j = 0..9, j != r.  Bit-identical to dk_sweep; per sweep ~2x fewer
+// instructions on the critical wave.  Runs a polynomial to the end (Brent exit,
+// no parking), as pass 0 of a round.
+template <int T>
+__device__ __forceinline__ double row_bcast(double v) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, 0x150 + T, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), 0x150 + T, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <int T>
+__device__ __forceinline__ void dkw_step(const Cx& num, Cx& den, Cx& mine, Cx (&roots)[10], int r, bool& moved_l,
+                                         bool& zero_l) {
+    if constexpr (T < 10) {
+        if (r == T) {
+#pragma unroll
+            for (int j = T + 1; j < 10; ++j) den = cmul(den, csub(mine, roots[j]));
+            zero_l = !(den.re != 0 || den.im != 0) || den.re != den.re || den.im != den.im;
+            const Cx q = cdiv(num, den);
+            mine = csub(mine, q);
+            moved_l = (q.re * q.re + q.im * q.im) > 0;
+        }
+        roots[T] = Cx{row_bcast<T>(mine.re), row_bcast<T>(mine.im)};
+        if (r > T) den = cmul(den, csub(mine, roots[T]));
+        dkw_step<T + 1>(num, den, mine, roots, r, moved_l, zero_l);
+    }
+}
+
+__global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pairs) {
+    const int lane = threadIdx.x, r = lane & 15, rowbase = lane & ~15;
+    const int total = g.dk_ctl[1];
+    const int item = blockIdx.x * 4 + (lane >> 4);
+    bool active = item < total;
+    double* R = nullptr;
+    if (active) {
+        int lo = 0, hi = pairs - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (g.dk_off[mid] <= item) lo = mid;
+            else hi = mid - 1;
+        }
+        R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
+        active = R[kRecGeneric * 64] == 0.0;  // else stage C runs the generic solver
+    }
+    if (__ballot(active) == 0) return;
+    double c[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) c[k] = active ? R[(kRecC + k) * 64] : 1.0;
+    Cx roots[10];
+    dk_init(roots);
+    Cx mine = roots[0];
+#pragma unroll
+    for (int k = 1; k < 10; ++k)
+        if (r == k) mine = roots[k];
+    Cx saved = mine;  // DkBrent::start
+    int it = 0, saved_it = 0, power = 1, target = 300;
+    const unsigned long long own = 0x3FFull << rowbase;  // the row's root lanes
+    for (;;) {
+        if (__ballot(active) == 0) break;
+        // one sweep (every lane runs it; finished rows' results are ignored)
+        Cx num{c[10], 0};
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+            const Cx t = cmul(num, mine);
+            num = Cx{t.re + c[10 - j - 1], t.im + 0.0};
+        }
+        Cx den{c[10], 0};
+        bool moved_l = false, zero_l = false;
+        dkw_step<0>(num, den, mine, roots, r, moved_l, zero_l);
+        const bool moved = (__ballot(moved_l && r < 10) & own) != 0;
+        const bool same = (__ballot(zero_l && r < 10) & own) != 0;
+        const bool eq_l = __builtin_bit_cast(long long, mine.re) == __builtin_bit_cast(long long, saved.re) &&
+                          __builtin_bit_cast(long long, mine.im) == __builtin_bit_cast(long long, saved.im);
+        const bool eq = (__ballot(eq_l || r >= 10) & own) == own;
+        if (!active) continue;
+        if (same) {  // coincident roots: stage C redoes this polynomial exactly
+            if (r == 0) R[kRecGeneric * 64] = 2.0;
+            active = false;
+            continue;
+        }
+        // DkBrent::step, identical in the row's lanes
+        ++it;
+        bool done = !moved || it >= target;
+        if (!done && target == 300) {
+            if (eq) {
+                target = it + (300 - it) % (it - saved_it);
+                done = it >= target;
+            } else if (it - saved_it == power) {
+                saved = mine;
+                saved_it = it;
+                power <<= 1;
+            }
+        }
+        if (done) {
+            if (r < 10) {
+                const double im = fabs(mine.im) < 1e-100 ? 0.0 : mine.im;  // dk_finish
+                R[(kRecRoots + 2 * r) * 64] = mine.re;
+                R[(kRecRoots + 2 * r + 1) * 64] = im;
+            }
+            if (r == 0) R[kRecNr * 64] = 10;
+            active = false;
+        }
+    }
+}
+
 // Stage C of every hypothesis of the round: models and their count.
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
     const int p = blockIdx.y;
@@ -1477,14 +1593,12 @@ __global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
     }
 }
 
-// A few pairs leave the GPU idle, so they take one round over every hypothesis
-// up to maxIters: one Durand-Kerner tail instead of two (the per-call
-// findEssentialMat of the drop-in surface: 2.3 -> ~1.2 ms).  Rounds only
-// schedule the same hypotheses; the replay's result is the same.
-constexpr int kOneRoundPairs = 4;
-hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
+// one = kStageOneRound (the per-call path): a single pair leaves the GPU idle,
+// so it takes one round over every hypothesis up to maxIters -- one
+// Durand-Kerner tail instead of two -- solved by ransac_dk_wide_kernel.
+// Rounds only schedule the same hypotheses; the replay's result is the same.
+hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) {
     const int cap = g.hyp_cap;
-    const bool one = pairs <= kOneRoundPairs;
     const int rounds = one ? 1 : kRansacRounds;
     for (int round = 0; round < rounds; ++round) {
         const int hi = one ? cap : kRansacBounds[round];
@@ -1495,10 +1609,15 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, hipStream_t s) {
         const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
         hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
         hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        const dim3 dgrid((unsigned)(((int64_t)pairs * span + kDkNT - 1) / kDkNT));
-        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 0, kDkBudget0);
-        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
-        hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
+        if (one) {
+            hipLaunchKernelGGL(ransac_dk_wide_kernel, dim3((unsigned)(((int64_t)pairs * span + 3) / 4)), dim3(64), 0, s, g,
+                               pairs);
+        } else {
+            const dim3 dgrid((unsigned)(((int64_t)pairs * span + kDkNT - 1) / kDkNT));
+            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 0, kDkBudget0);
+            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
+            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
+        }
         hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
         hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
                            s, g);
@@ -1895,7 +2014,7 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
     if (pairs <= 0) return hipSuccess;
     if (stages & kStageNormalize) hipLaunchKernelGGL(normalize_kernel, dim3(4, pairs), dim3(256), 0, s, g);
     if (stages & kStageRansac) {
-        hipError_t e = launch_ransac(g, pairs, s);
+        hipError_t e = launch_ransac(g, pairs, (stages & kStageOneRound) != 0, s);
         if (e != hipSuccess) return e;
     }
     if (stages & kStagePose) {
