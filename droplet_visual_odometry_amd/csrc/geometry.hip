@@ -985,12 +985,57 @@ constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
 // one wave per pair: idx[i] = rng.uniform(0, m) = rng.next() % m, redrawn
 // while it repeats an earlier index of the subset.  The MWC stream itself is
-// sequential (lane 0 runs it into LDS, one v_mad_u64_u32 per state), the
+// sequential, but a multiply-with-carry stream can be jumped ahead (below), the
 // subsets are assembled 64 at a time: lane j takes the 5 states after the
 // 5j consumed before it, which is exact unless an earlier lane drew a
 // duplicate; the first such lane redoes its subset with the rejection loop
-// (wave-uniform, ~1% of subsets) and the next 64 start after it.
+// (wave-uniform, ~1% of subsets) and the next 64 start after it.  The stream
+// is staged 1,024 states at a time, 64 lanes jumping ahead (below).
 constexpr int kSampleBuf = 1024;  // MWC states staged per refill
+
+// Jump-ahead of cv::RNG's multiply-with-carry step s' = (u32)s * A + (s >> 32),
+// A = 4164903690.  With m = A * 2^32 - 1, s' * 2^32 = s + (u32)s * m, so
+// s' = s * A (mod m) (A = 2^-32 mod m), and a state below m stays below m: from
+// the second state of a stream on (the seed ~0 is the only state >= m it
+// meets), s_{n+k} = s_n * A^k mod m exactly.  Lane j of a refill starts from
+// s_n * A^(16 j + 1), a Montgomery product (R = 2^64) with the table below,
+// and steps 15 times; the buffer equals lane 0 running the stream sequentially.
+constexpr uint64_t kMwcA = 4164903690ull;
+constexpr uint64_t kMwcM = kMwcA * (1ull << 32) - 1;
+constexpr uint64_t mwc_mprime() {  // -m^-1 mod 2^64 (Newton)
+    uint64_t inv = kMwcM;
+    for (int i = 0; i < 6; ++i) inv *= 2 - kMwcM * inv;
+    return 0 - inv;
+}
+constexpr uint64_t kMwcMp = mwc_mprime();
+struct MwcJump {
+    uint64_t v[64];  // A^(16 j + 1) * 2^64 mod m
+};
+constexpr MwcJump mwc_jump() {
+    MwcJump t{};
+    unsigned __int128 p = kMwcA % kMwcM;  // A^1
+    unsigned __int128 a16 = 1;
+    for (int i = 0; i < 16; ++i) a16 = a16 * kMwcA % kMwcM;
+    for (int j = 0; j < 64; ++j) {
+        t.v[j] = (uint64_t)((p << 64) % kMwcM);
+        p = p * a16 % kMwcM;
+    }
+    return t;
+}
+__constant__ MwcJump c_mwc_jump = mwc_jump();
+static_assert(kMwcM % 2 == 1 && (uint64_t)(kMwcM * (0 - kMwcMp)) == 1, "Montgomery constants");
+
+__device__ __forceinline__ uint64_t mwc_mont(uint64_t a, uint64_t bR) {  // a * b mod m, a < m, bR = b * 2^64 mod m
+    const uint64_t lo = a * bR, hi = __umul64hi(a, bR);
+    const uint64_t u = lo * kMwcMp;
+    const uint64_t uh = __umul64hi(u, kMwcM);
+    uint64_t t = hi + uh;
+    const bool c1 = t < hi;
+    const uint64_t c = lo != 0;  // lo + u * m = 0 mod 2^64, with a carry unless lo == 0
+    const uint64_t t2 = t + c;
+    const bool c2 = t2 < t;
+    return (c1 || c2 || t2 >= kMwcM) ? t2 - kMwcM : t2;
+}
 __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round, int bound) {
     const int p = blockIdx.x;
     if (p >= pairs) return;
@@ -1041,11 +1086,23 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
 #pragma unroll
         for (int k = 0; k < kSampleBuf / 64; ++k)
             if (64 * k + lane < keep) s_st[64 * k + lane] = tmp[k];
+        const int head = min(2, kSampleBuf - keep);  // sequential: the stream's first state may be >= m
         if (lane == 0) {
             uint64_t st = gen;
-            for (int k = keep; k < kSampleBuf; ++k) {
-                st = (uint64_t)(uint32_t)st * 4164903690U + (st >> 32);
+            for (int k = keep; k < keep + head; ++k) {
+                st = (uint64_t)(uint32_t)st * kMwcA + (st >> 32);
                 s_st[k] = st;
+            }
+        }
+        __syncthreads();
+        const int rest = kSampleBuf - keep - head;  // the remaining states by jump-ahead, 16 per lane
+        if (16 * lane < rest) {
+            const int k0 = keep + head + 16 * lane;
+            uint64_t st = mwc_mont(s_st[keep + head - 1], c_mwc_jump.v[lane]);
+            s_st[k0] = st;
+            for (int q = 1; q < 16 && k0 + q < kSampleBuf; ++q) {
+                st = (uint64_t)(uint32_t)st * kMwcA + (st >> 32);
+                s_st[k0 + q] = st;
             }
         }
         __syncthreads();
