@@ -113,8 +113,18 @@ __global__ __launch_bounds__(256) void col_scan_kernel(SurfArgs a) {
     const int sw = a.w + 1;
     if (x > a.w) return;
     a.sum[x] = 0;
-    int acc = 0;
-    for (int y = 1; y <= a.h; ++y) {
+    int acc = 0, y = 1;
+    for (; y + 8 <= a.h + 1; y += 8) {  // 8 rows of loads in flight, then the sequential sums
+        int v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = a.sum[(size_t)(y + k) * sw + x];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc += v[k];
+            a.sum[(size_t)(y + k) * sw + x] = acc;
+        }
+    }
+    for (; y <= a.h; ++y) {
         acc += a.sum[(size_t)y * sw + x];
         a.sum[(size_t)y * sw + x] = acc;
     }
@@ -464,14 +474,25 @@ __global__ __launch_bounds__(64) void describe_kernel(SurfArgs a) {
                 float* buf = s_buf[lane];
                 for (int dx = 0; dx < kP1; ++dx) buf[dx] = 0;
                 double px = s_sx[sy], py = s_sy[sy];
-                for (int x = 0; x < n; ++x, px += cos_dir, py -= sin_dir) {
-                    const uint8_t v = win_sample(a, px, py);
-                    if (fast) {
-                        reinterpret_cast<int*>(buf)[x / iscale] += v;
-                    } else {
-                        const int e0 = s_e0[x], e1 = s_e1[x];
-                        if (e0 >= 0) buf[e0] += v * s_a0[x];
-                        if (e1 >= 0) buf[e1] += v * s_a1[x];
+                for (int x0 = 0; x0 < n; x0 += 8) {  // 8 samples' image reads in flight
+                    uint8_t v[8];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        v[q] = x0 + q < n ? win_sample(a, px, py) : 0;
+                        px += cos_dir;  // the reference's per-pixel accumulation (done for the
+                        py -= sin_dir;  // padding samples too: they are never read back)
+                    }
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int x = x0 + q;
+                        if (x >= n) break;
+                        if (fast) {
+                            reinterpret_cast<int*>(buf)[x / iscale] += v[q];
+                        } else {
+                            const int e0 = s_e0[x], e1 = s_e1[x];
+                            if (e0 >= 0) buf[e0] += v[q] * s_a0[x];
+                            if (e1 >= 0) buf[e1] += v[q] * s_a1[x];
+                        }
                     }
                 }
             }
@@ -565,12 +586,16 @@ __global__ __launch_bounds__(kSortNT) void compact_kernel(SurfArgs a) {
     }
     __syncthreads();
     int pos = s_part[threadIdx.x];
-    for (int i = i0; i < i1; ++i)
-        if (a.kps[i].size > 0) {
-            a.out[pos] = a.kps[i];
-            for (int q = 0; q < 64; ++q) a.desc[(size_t)pos * 64 + q] = a.dtmp[(size_t)i * 64 + q];
-            ++pos;
-        }
+    for (int i = i0; i < i1; ++i) {  // destination of each kept keypoint (order: a.order, free after the sort)
+        const bool keep = a.kps[i].size > 0;
+        a.order[i] = keep ? pos : -1;
+        if (keep) a.out[pos++] = a.kps[i];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n * 64; e += kSortNT) {  // descriptors: flat, coalesced
+        const int i = e >> 6, d = a.order[i];
+        if (d >= 0) a.desc[(size_t)d * 64 + (e & 63)] = a.dtmp[e];
+    }
 }
 
 }  // namespace
