@@ -24,7 +24,7 @@ constexpr int kMaxLevels = 8;
 #define DVO_BAND_ROWS 24
 #endif
 constexpr int kBandRows = DVO_BAND_ROWS;
-constexpr int kFastTW = 126;        // FAST tile width (output columns; score window 128)
+constexpr int kFastTW = 124;        // FAST tile width (output columns; score columns 126 = LDS words 1..32)
 constexpr int kBorder = 31;         // edgeThreshold == runByImageBorder border
 constexpr int kMaxW = 4096;         // keys pack x, y in 12 bits each
 #ifndef DVO_BLUR_TH

@@ -478,13 +478,13 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 }
 
 // FAST over one column strip of one level.  The workgroup walks the strip's
-// tiles (kBandRows output rows x kFastTW (126) output columns) top to bottom.
+// tiles (kBandRows output rows x kFastTW (124) output columns) top to bottom.
 // The image window of a tile (rows [r0-4, r0+kBandRows+4), 144 columns from the
-// aligned column bx) lives in LDS as words; the next tile's kBandRows new rows are loaded into
+// column bx = xs - 7) lives in LDS as words; the next tile's kBandRows new rows are loaded into
 // registers while the current tile is processed (the load latency hides behind
 // the compute), and its last 8 rows are carried to the top of the window, so
 // every image byte is fetched from HBM once.  FAST scores are needed on the
-// NMS neighbourhood, score rows [r0-1, r1] x score columns [xs-1, xs+127): the
+// NMS neighbourhood, score rows [r0-1, r1] x score columns [xs-1, xs+125): the
 // first tile computes all kBandRows+2 score rows, later tiles the kBandRows new ones and carry
 // the two above (and the corners of the last one, an output row of the next
 // tile, in a small list).  Per tile, phases separated by workgroup barriers;
@@ -493,6 +493,9 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //   compass  every pixel: a run of 9 on the 16-circle contains two adjacent
 //            compass pixels (0,4 / 4,8 / 8,12 / 12,0) that are both brighter
 //            or both darker: min(max(c0,c8), max(c4,c12)) > v+t, or the dual;
+//            a lane tests the 4 pixels of one LDS word from 5 word reads
+//            (centre row -1/0/+1 words, rows -3/+3), byte-permuted into packed
+//            u16 pairs and compared with saturating v_pk ops;
 //   segment  survivors (~6%): the 16 circle compares packed into bright/dark
 //            masks with v_alignbit (sign bit shifted in), run-of-9 test;
 //   score    corners (~1%): cornerScore<16> into the LDS score plane;
@@ -501,7 +504,11 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //            row; select_fast_kernel restores raster order across tiles.
 constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
 constexpr int kFtRows = kBandRows + 8;          // staged image rows per tile: [r0-4, r0+kBandRows+4)
-constexpr int kFtSeg = ((kBandRows + 2 + 3) / 4) * 128;  // per-wave list capacity (score rows sr == wid mod 4)
+static_assert(kFastTW == 124 && (kBorder - 7) % 4 == 0, "FAST tiles: score columns = LDS words 1..32");
+// per-wave list capacities: compass, row pairs wid, wid+4, .. of 64 lanes x 4 px; segment test, the
+// concatenated candidates of the tile (<= (kBandRows + 2) x 126) in 64-lane rounds of the 4 waves
+constexpr int kFtSegCand = ((kBandRows + 3) / 2 + 3) / 4 * 256;
+constexpr int kFtSegCorner = ((kBandRows + 2) * 126 + 255) / 256 * 64;
 constexpr int kFtWords = kFtLW / 4;             // words per staged row
 constexpr int kFtNewW = kBandRows * kFtWords;   // words loaded per tile (rows r0+4 .. r0+kBandRows+4)
 constexpr int kFtPf = (kFtNewW + kFastNT - 1) / kFastNT;
@@ -509,10 +516,20 @@ constexpr int kFtCarryW = 8 * kFtWords;         // image words carried (the wind
 constexpr int kFtCarryR = (kFtCarryW + kFastNT - 1) / kFastNT;
 constexpr int kFtCarryList = 128;               // corners of one score row
 static_assert(kFtRows * kFtWords == kFtNewW + kFtCarryW, "staging covers the window");
+// The compass pre-test of two pixels (packed u16 pairs): min(max(c0,c8), max(c4,c12)) - v > t or
+// v - max(min(c0,c8), min(c4,c12)) > t, as saturating differences (t in [0, 255]); a nonzero
+// half (<= 255) passes.
+__device__ __forceinline__ uint32_t compass_pass(u16x2 v, u16x2 c0, u16x2 c8, u16x2 c4, u16x2 c12, uint32_t thr2) {
+    const u16x2 X = __builtin_elementwise_min(__builtin_elementwise_max(c0, c8), __builtin_elementwise_max(c4, c12));
+    const u16x2 Y = __builtin_elementwise_max(__builtin_elementwise_min(c0, c8), __builtin_elementwise_min(c4, c12));
+    const u16x2 m = __builtin_elementwise_max(__builtin_elementwise_sub_sat(X, v), __builtin_elementwise_sub_sat(v, Y));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(m, as_u16x2(thr2)));
+}
 __device__ __forceinline__ uint32_t lane_prefix(unsigned long long bal) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
 }
 // entry e of the concatenation of the 4 per-wave segments of `list` (counts cnt[0..3])
+template <int kSeg>
 __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int e) {
     int s = 0;
 #pragma unroll
@@ -522,7 +539,7 @@ __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int 
         s += past ? 1 : 0;
         if (!past) break;
     }
-    return list[s * kFtSeg + e];
+    return list[s * kSeg + e];
 }
 
 __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
@@ -535,7 +552,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     const int c = strip - G.strip_base;
     const int w = G.w, h = G.h;
     const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
-    const int bx = (xs - 4) & ~3;  // image column of LDS column 0; xs - bx in [4, 7]
+    const int bx = xs - 7;  // image column of LDS column 0 (a multiple of 4: kBorder - 7 and kFastTW are)
     const int thr = P.plan.fast_threshold;
     const uint8_t* src = level_ptr(P, f, l);
     const int sp = level_pitch(P, l);
@@ -543,18 +560,23 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+kBandRows+4)
     __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+kBandRows+1)
     // + 64 slots per wave that lanes without an entry store to (branch-free appends: no exec-mask SALU)
-    __shared__ uint16_t cand[4 * kFtSeg + 256], corner[4 * kFtSeg + 256];
+    __shared__ uint16_t cand[4 * kFtSegCand + 256], corner[4 * kFtSegCorner + 256];
     __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
     __shared__ int ncand[4], ncorner[4], ncarry[2];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
     __shared__ int row_off[4][kBandRows];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int x_lo = xs - 1 + lane;
     const int xlast = min(xe, w - 4);  // last score column (xs - 1 >= 30 >= 3 on the left)
-    const bool ok0 = x_lo <= xlast, ok1 = x_lo + 64 <= xlast;
+    // score columns [xs - 1, xlast] are LDS columns [6, xlast - bx + 1) <= [6, 132): the LDS words
+    // 1..32 of a row; this lane's word and the mask of its score bytes
+    const int c_col = 4 + 4 * (lane & 31), c_hi = xlast - bx + 1 - c_col;
+    const uint32_t c_vm = (c_col == 4 ? 0xFFFF0000u : 0xFFFFFFFFu) &
+                          (c_hi >= 4 ? 0xFFFFFFFFu : c_hi <= 0 ? 0u : (1u << (8 * c_hi)) - 1u);
+    const uint32_t thr2 = (uint32_t)thr * 0x10001u;
     // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
-    // load returns whatever lies there (or 0 past the level).
+    // load returns whatever lies there (or 0 past the level).  The row offset goes in the
+    // per-lane offset: the rows of one wave's words differ (a scalar offset would be a waterfall).
     uint32_t creg[kFtCarryR], pf[kFtPf], screg = 0;
     {  // prologue: rows [r0-4, r0+4) into the carry registers, [r0+4, r0+kBandRows+4) into the prefetch registers
         const int ylo = kBorder - 4;
@@ -562,13 +584,13 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         for (int k = 0; k < kFtCarryR; ++k) {
             const int q = threadIdx.x + k * kFastNT;
             const int rr = q / kFtWords, wd = q - rr * kFtWords;
-            creg[k] = q < kFtCarryW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + rr) * sp, 0) : 0u;
+            creg[k] = q < kFtCarryW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd + (ylo + rr) * sp, 0, 0) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < kFtPf; ++k) {
             const int q = threadIdx.x + k * kFastNT;
             const int rr = q / kFtWords, wd = q - rr * kFtWords;
-            pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ylo + 8 + rr) * sp, 0) : 0u;
+            pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd + (ylo + 8 + rr) * sp, 0, 0) : 0u;
         }
     }
     if (threadIdx.x == 0) ncarry[0] = 0;
@@ -607,41 +629,45 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             for (int k = 0; k < kFtPf; ++k) {
                 const int q = threadIdx.x + k * kFastNT;
                 const int rr = q / kFtWords, wd = q - rr * kFtWords;
-                pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd, (ynew + rr) * sp, 0)
+                pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, bx + 4 * wd + (ynew + rr) * sp, 0, 0)
                                     : 0u;
             }
         }
-        // ---- compass: score rows sr == wid (mod 4) into this wave's candidate segment
+        // ---- compass, four score pixels per lane: lane -> LDS word 1 + (lane & 31) of score row
+        // sr_lo + 2 (wid + 4 t) + (lane >> 5), t = 0, 1, ...
         const int nsr = nrows + 2;
         const int sr_lo = b == 0 ? 0 : 2;
         {
-            const int seg_off = wid * kFtSeg, spare_i = 4 * kFtSeg + wid * 64 + lane;
-            const uint32_t okm = (ok0 ? 1u : 0u) | (ok1 ? 2u : 0u);
+            const int seg_off = wid * kFtSegCand, spare_i = 4 * kFtSegCand + wid * 64 + lane;
             int n = 0;  // wave-uniform
-            // interior strips (every score column valid) skip the column mask
-            auto rows = [&](auto interior) {
-                for (int sr = sr_lo + ((wid - sr_lo) & 3); sr < nsr; sr += kFastNT / 64) {
-                    const int a = (sr + 3) * kFtLW + (x_lo - bx);
+            for (int sr = sr_lo + 2 * wid + (lane >> 5); __builtin_amdgcn_readfirstlane(sr - (lane >> 5)) < nsr;
+                 sr += 8) {
+                const int base = (sr + 3) * kFtLW + c_col;  // centre-row byte address of the word
+                const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + base);
+                const uint32_t wc = wp[0], wl = wp[-1], wr = wp[1];
+                const uint32_t wu = wp[-3 * kFtWords], wd = wp[3 * kFtWords];
+                // pixels 0, 2 in the low pair, 1, 3 in the high pair; c4 = columns +3, c12 = columns -3
+                const uint32_t r0p = compass_pass(as_u16x2(__builtin_amdgcn_perm(0, wc, 0x0C020C00)),
+                                                  as_u16x2(__builtin_amdgcn_perm(0, wu, 0x0C020C00)),
+                                                  as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C020C00)),
+                                                  as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C050C03)),
+                                                  as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C030C01)), thr2);
+                const uint32_t r1p = compass_pass(as_u16x2(__builtin_amdgcn_perm(0, wc, 0x0C030C01)),
+                                                  as_u16x2(__builtin_amdgcn_perm(0, wu, 0x0C030C01)),
+                                                  as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C030C01)),
+                                                  as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C060C04)),
+                                                  as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C040C02)), thr2);
+                // byte k of pm nonzero <=> pixel k passes and is a score pixel of this tile
+                const uint32_t pm = (r0p | (r1p << 8)) & (sr < nsr ? c_vm : 0u);
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const int ah = a + 64 * hh;
-                        const int v = img[ah];
-                        const int c0 = img[ah + 3 * kFtLW], c4 = img[ah + 3], c8 = img[ah - 3 * kFtLW], c12 = img[ah - 3];
-                        // the whole condition as integer arithmetic: max(X - v, v - Y) > t from a sign bit
-                        // (no compare masks, no exec changes); one compare for the ballot; the store
-                        // address selected (lanes that do not pass write their spare slot)
-                        const int X = min(max(c0, c8), max(c4, c12)), Y = max(min(c0, c8), min(c4, c12));
-                        uint32_t pm = (uint32_t)(thr - max(X - v, v - Y)) >> 31;
-                        if (!decltype(interior)::value) pm &= okm >> hh;
-                        const unsigned long long bal = __ballot(pm != 0);
-                        const int to = seg_off + n + (int)lane_prefix(bal);
-                        cand[pm ? to : spare_i] = (uint16_t)ah;
-                        n += __popcll(bal);
-                    }
+                for (int k = 0; k < 4; ++k) {
+                    const bool pass = ((pm >> (8 * k)) & 0xFF) != 0;
+                    const unsigned long long bal = __ballot(pass);
+                    const int to = seg_off + n + (int)lane_prefix(bal);
+                    cand[pass ? to : spare_i] = (uint16_t)(base + k);
+                    n += __popcll(bal);
                 }
-            };
-            if (__ballot(okm != 3) == 0) rows(std::true_type{});  // wave-uniform choice
-            else rows(std::false_type{});
+            }
             if (lane == 0) ncand[wid] = n;
         }
         __syncthreads();
@@ -651,15 +677,15 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
             const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-            uint16_t* seg = corner + wid * kFtSeg;
-            uint16_t* const spare = corner + 4 * kFtSeg + wid * 64 + lane;
+            uint16_t* seg = corner + wid * kFtSegCorner;
+            uint16_t* const spare = corner + 4 * kFtSegCorner + wid * 64 + lane;
             int n = 0;
             for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
                 const int e = e0 + lane;
                 bool is_corner = false;
                 int a = 0;
                 if (e < total) {
-                    a = seg_at(cand, cnt, e);
+                    a = seg_at<kFtSegCand>(cand, cnt, e);
                     const uint8_t* p = img + a;
                     const int v = p[0];
                     const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
@@ -686,7 +712,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         const int nc = ncarry[par];
         // ---- scores of the new corners into the score plane
         for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
-            const int a = seg_at(corner, cnt2, e);
+            const int a = seg_at<kFtSegCorner>(corner, cnt2, e);
             const uint8_t* p = img + a;
             int cc[16];
 #pragma unroll
@@ -699,7 +725,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         // ---- strict 3x3 NMS of the carried and new corners; keeps lie in rows [r0, r1), columns [xs, xe).
         // New corners of score row kBandRows+1 (row r0 + kBandRows) are the next tile's row-1 corners.
         for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
-            const int a = (e < nc ? (int)carry[par][e] : seg_at(corner, cnt2, e - nc)) - 3 * kFtLW;  // score-plane address
+            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCorner>(corner, cnt2, e - nc)) - 3 * kFtLW;  // score-plane address
             const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
             if (sr == kBandRows + 1) {
                 const int slot = atomicAdd(&ncarry[par ^ 1], 1);
@@ -743,7 +769,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
-            const int a = (e < nc ? (int)carry[par][e] : seg_at(corner, cnt2, e - nc)) - 3 * kFtLW;
+            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCorner>(corner, cnt2, e - nc)) - 3 * kFtLW;
             const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
             if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
             const int i_col = x - (xs - 1), wq = i_col >> 5;
