@@ -1034,8 +1034,16 @@ __device__ int retain_best_block(const A& a, int n, int npoints, int depth, int3
 #define DVO_SEL_NT 128  // measured: 128 threads 0.81 ms, 256 0.82, 512 1.06, 1024 2.17 (select + Harris, 513 frames)
 #endif
 constexpr int kSelNT = DVO_SEL_NT;
+// Batches of a few frames (the per-call drop-in surface: one frame) are latency-bound:
+// fewer, wider partition chunks.  Drop-in pairs/s at 1280x720 (tools/ab_dropin.sh):
+// 128 threads 429, 256 441, 512 452, 1024 447.
+#ifndef DVO_SEL_NT_CALL
+#define DVO_SEL_NT_CALL 512
+#endif
+constexpr int kSelNTCall = DVO_SEL_NT_CALL, kSelCallFrames = 4;
 
-__global__ __launch_bounds__(kSelNT) void select_fast_kernel(StreamParams P) {
+template <int NT>
+__global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
     const int l = blockIdx.x, f = blockIdx.y;
     if (l >= P.plan.nlevels) return;
     const LevelGeom& G = P.plan.L[l];
@@ -1048,7 +1056,7 @@ __global__ __launch_bounds__(kSelNT) void select_fast_kernel(StreamParams P) {
     const int nseg = G.nbands * kBandRows * G.ntx;
     if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
-    for (int s0 = 0; s0 < nseg; s0 += kSelNT) {
+    for (int s0 = 0; s0 < nseg; s0 += NT) {
         const int sg = s0 + threadIdx.x;
         int cnt = 0, src_off = 0;
         if (sg < nseg) {
@@ -1149,7 +1157,8 @@ __global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
     }
 }
 
-__global__ __launch_bounds__(kSelNT) void select_harris_kernel(StreamParams P) {
+template <int NT>
+__global__ __launch_bounds__(NT) void select_harris_kernel(StreamParams P) {
     const int l = blockIdx.x, f = blockIdx.y;
     if (l >= P.plan.nlevels) return;
     const LevelGeom& G = P.plan.L[l];
@@ -1412,9 +1421,15 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
         hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
-    hipLaunchKernelGGL(select_fast_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    if (F <= kSelCallFrames)
+        hipLaunchKernelGGL(select_fast_kernel<kSelNTCall>, dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
+    else
+        hipLaunchKernelGGL(select_fast_kernel<kSelNT>, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     hipLaunchKernelGGL(harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(select_harris_kernel, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+    if (F <= kSelCallFrames)
+        hipLaunchKernelGGL(select_harris_kernel<kSelNTCall>, dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
+    else
+        hipLaunchKernelGGL(select_harris_kernel<kSelNT>, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
     hipLaunchKernelGGL(describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
