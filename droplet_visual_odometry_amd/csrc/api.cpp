@@ -8,6 +8,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -45,6 +46,9 @@ struct dvo_ctx {
     std::vector<std::pair<void*, size_t>> scratch;
     dvo_stream* call_stream = nullptr;  // cached plan for detectAndCompute
     int call_w = 0, call_h = 0, call_nf = 0;
+    // grow-only pinned host staging of the synchronous per-call entry points
+    uint8_t* pin = nullptr;
+    size_t pin_cap = 0;
 };
 
 struct dvo_stream {
@@ -215,6 +219,54 @@ int dalloc(dvo_stream* s, T** p, size_t n) {
 }
 
 // grow-only per-context scratch slot
+// One synchronous per-call operation's host traffic through pinned memory: inputs are
+// packed into the staging area and sent with asynchronous copies on the call's
+// stream, outputs come back the same way, and the caller synchronises once (a
+// pageable hipMemcpy is a blocking staged copy each: ~10-20 us apiece).
+struct Staging {
+    uint8_t* base = nullptr;
+    size_t off = 0, cap = 0;
+    hipStream_t s = nullptr;
+    static size_t round(size_t n) { return (n + 63) & ~(size_t)63; }
+    uint8_t* take(size_t n) {  // the next n staged bytes (64-byte aligned)
+        uint8_t* h = base + off;
+        off += round(n);
+        if (off > cap) {  // a caller sized its staging() request wrong: never write past the area
+            std::fprintf(stderr, "dvo: staging overflow (%zu > %zu)\n", off, cap);
+            std::abort();
+        }
+        return h;
+    }
+    hipError_t send(void* dev, const uint8_t* h, size_t n) {  // host -> device of staged bytes
+        return n ? hipMemcpyAsync(dev, h, n, hipMemcpyHostToDevice, s) : hipSuccess;
+    }
+    hipError_t put(void* dev, const void* src, size_t n) {
+        uint8_t* h = take(n);
+        if (n) std::memcpy(h, src, n);
+        return send(dev, h, n);
+    }
+    hipError_t get(const void* dev, size_t n, uint8_t** h) {  // device -> host, valid after synchronising
+        *h = take(n);
+        return n ? hipMemcpyAsync(*h, dev, n, hipMemcpyDeviceToHost, s) : hipSuccess;
+    }
+};
+
+static int staging(dvo_ctx* ctx, size_t bytes, hipStream_t s, Staging* st) {
+    if (ctx->pin_cap < bytes) {
+        if (ctx->pin) HIP_TRY(hipHostFree(ctx->pin));
+        ctx->pin = nullptr;
+        ctx->pin_cap = 0;
+        const size_t nb = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+        HIP_TRY(hipHostMalloc((void**)&ctx->pin, nb, hipHostMallocDefault));
+        ctx->pin_cap = nb;
+    }
+    st->base = ctx->pin;
+    st->off = 0;
+    st->cap = ctx->pin_cap;
+    st->s = s;
+    return DVO_OK;
+}
+
 int scratch(dvo_ctx* ctx, int slot, size_t bytes, void** out) {
     if ((int)ctx->scratch.size() <= slot) ctx->scratch.resize(slot + 1, {nullptr, 0});
     auto& e = ctx->scratch[slot];
@@ -439,6 +491,7 @@ void dvo_ctx_destroy(dvo_ctx* ctx) {
     if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
     for (auto& e : ctx->scratch)
         if (e.first) hipFree(e.first);
+    if (ctx->pin) hipHostFree(ctx->pin);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -691,10 +744,32 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
     }
     dvo_stream* s = ctx->call_stream;
     const int pw = frame_pitch(s);
+    const size_t kc = (size_t)s->plan.kp_cap;
+    Staging st;
+    if ((rc = staging(ctx, 2 * Staging::round(4) + Staging::round(kc * sizeof(dvo_keypoint)) + Staging::round(kc * 32),
+                      s->hs, &st)))
+        return rc;
     HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, img, stride, w, h, hipMemcpyHostToDevice, s->hs));
     rc = run_stream(s, s->d_frames, 1, (int64_t)pw * h, pw, nullptr, true);
     if (rc) return rc;
-    return dvo_stream_get_features(s, 0, kps, desc, cap, n_out);
+    // dvo_stream_get_features of frame 0, with every list copied back at once (capacity-sized)
+    uint8_t *hn, *hst, *hk = nullptr, *hd = nullptr;
+    HIP_TRY(st.get(s->buf.nkp, sizeof(int), &hn));
+    HIP_TRY(st.get(s->buf.status, sizeof(int), &hst));
+    if (kps) HIP_TRY(st.get(s->buf.kps, kc * sizeof(dvo_keypoint), &hk));
+    if (desc) HIP_TRY(st.get(s->buf.desc, kc * 32, &hd));
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    int nk = 0, stt = 0;
+    std::memcpy(&nk, hn, sizeof(int));
+    std::memcpy(&stt, hst, sizeof(int));
+    *n_out = nk;
+    if (stt) return fail(ctx, DVO_ECAP, "keypoint capacity exceeded (Harris ties)");
+    if (nk > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
+    if (nk > 0) {
+        if (kps) std::memcpy(kps, hk, sizeof(dvo_keypoint) * nk);
+        if (desc) std::memcpy(desc, hd, 32 * (size_t)nk);
+    }
+    return DVO_OK;
 }
 
 int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t* dt, int nt, int cross_check,
@@ -714,16 +789,23 @@ int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t*
         (rc = scratch(ctx, 3, (size_t)nq * sizeof(dvo_dmatch), &bout)) ||
         (rc = scratch(ctx, 4, 64, &bm)))
         return rc;
-    HIP_TRY(hipMemcpyAsync(bq, dq, (size_t)nq * 32, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(bt, dt, (size_t)nt * 32, hipMemcpyHostToDevice, ctx->stream));
+    Staging st;
+    if ((rc = staging(ctx, Staging::round((size_t)nq * 32) + Staging::round((size_t)nt * 32) + Staging::round(64) +
+                               Staging::round((size_t)nq * sizeof(dvo_dmatch)), ctx->stream, &st)))
+        return rc;
+    HIP_TRY(st.put(bq, dq, (size_t)nq * 32));
+    HIP_TRY(st.put(bt, dt, (size_t)nt * 32));
     HIP_TRY(launch_match_pair((const uint8_t*)bq, nq, (const uint8_t*)bt, nt, cross_check, bnn, (dvo_dmatch*)bout,
                               (int*)bm, ctx->stream));
-    int m = 0;
-    HIP_TRY(hipMemcpyAsync(&m, bm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    uint8_t *hm, *hout;
+    HIP_TRY(st.get(bm, sizeof(int), &hm));
+    HIP_TRY(st.get(bout, (size_t)nq * sizeof(dvo_dmatch), &hout));  // at most one match per query
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int m = 0;
+    std::memcpy(&m, hm, sizeof(int));
     *m_out = m;
     if (m > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
-    if (m) HIP_TRY(hipMemcpy(out, bout, (size_t)m * sizeof(dvo_dmatch), hipMemcpyDeviceToHost));
+    if (m) std::memcpy(out, hout, (size_t)m * sizeof(dvo_dmatch));
     return DVO_OK;
 }
 
@@ -1029,17 +1111,17 @@ int dvo_sift_detect_and_compute(dvo_ctx* ctx, const uint8_t* img, int w, int h, 
     return DVO_OK;
 }
 
-static int upload_points(dvo_ctx* ctx, const double* p1, const double* p2, int m, void** dpts) {
+static int upload_points(dvo_ctx* ctx, Staging& st, const double* p1, const double* p2, int m, void** dpts) {
     int rc = scratch(ctx, 5, (size_t)(m > 0 ? m : 1) * 32, dpts);
     if (rc) return rc;
-    std::vector<double> h((size_t)m * 4);
+    double* h = reinterpret_cast<double*>(st.take((size_t)m * 32));
     for (int i = 0; i < m; ++i) {
         h[4 * i] = p1[2 * i];
         h[4 * i + 1] = p1[2 * i + 1];
         h[4 * i + 2] = p2[2 * i];
         h[4 * i + 3] = p2[2 * i + 1];
     }
-    if (m) HIP_TRY(hipMemcpy(*dpts, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(st.send(*dpts, reinterpret_cast<const uint8_t*>(h), (size_t)m * 32));
     return DVO_OK;
 }
 
@@ -1054,14 +1136,19 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *dgs, *drec, *doff, *dctl, *dlist;
     int rc;
     const size_t hc = (size_t)(max_iters > 1 ? max_iters : 1);
-    if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)m * 32, &dn)) ||
+    Staging st;
+    if ((rc = staging(ctx, Staging::round((size_t)m * 32) + Staging::round(16) + Staging::round(90 * 8) +
+                               Staging::round((size_t)m), ctx->stream, &st)))
+        return rc;
+    if ((rc = scratch(ctx, 6, (size_t)m * 32, &dn)) ||
         (rc = scratch(ctx, 7, hc * 90 * 8, &dmod)) || (rc = scratch(ctx, 8, 90 * 8, &dE)) ||
         (rc = scratch(ctx, 9, 16, &dinfo)) || (rc = scratch(ctx, 10, (size_t)m, &dmask)) ||
         (rc = scratch(ctx, 16, hc * 4, &dnmod)) || (rc = scratch(ctx, 17, hc * 40, &dcnt)) ||
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 20, ((hc + 63) / 64) * 200 * 64 * 8, &dgs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
-        (rc = scratch(ctx, 23, 16, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)))
+        (rc = scratch(ctx, 23, 16, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
+        (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
         return rc;
     GeomArgs g{};
     g.pts_d = (const double*)dpts;
@@ -1091,13 +1178,17 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.info = (int32_t*)dinfo;
     g.mask = (uint8_t*)dmask;
     HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStageRansac | kStageOneRound, ctx->stream));
-    int info[4];
-    HIP_TRY(hipMemcpyAsync(info, dinfo, sizeof(info), hipMemcpyDeviceToHost, ctx->stream));
+    uint8_t *hinfo, *hE, *hmask = nullptr;
+    HIP_TRY(st.get(dinfo, 16, &hinfo));
+    HIP_TRY(st.get(dE, 90 * 8, &hE));  // every row the kernel may write (<= 10 models)
+    if (mask) HIP_TRY(st.get(dmask, (size_t)m, &hmask));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    int info[4];
+    std::memcpy(info, hinfo, sizeof(info));
     if (info[3] != DVO_OK) return fail(ctx, info[3], "findEssentialMat: no model (E is empty)");
     *e_rows = info[0];
-    HIP_TRY(hipMemcpy(E, dE, sizeof(double) * 3 * info[0], hipMemcpyDeviceToHost));
-    if (mask) HIP_TRY(hipMemcpy(mask, dmask, (size_t)m, hipMemcpyDeviceToHost));
+    std::memcpy(E, hE, sizeof(double) * 3 * info[0]);
+    if (mask) std::memcpy(mask, hmask, (size_t)m);
     return DVO_OK;
 }
 
@@ -1111,18 +1202,24 @@ int dvo_recover_pose(dvo_ctx* ctx, const double* E, int e_rows, const double* p1
     void *dpts, *dn, *dE, *dinfo, *dRt, *dgood, *dpick, *dpm, *dmin = nullptr;
     int rc;
     const int mm = m > 0 ? m : 1;
-    if ((rc = upload_points(ctx, p1, p2, m, &dpts)) || (rc = scratch(ctx, 6, (size_t)mm * 32, &dn)) ||
+    Staging st;
+    if ((rc = staging(ctx, Staging::round((size_t)m * 32) + Staging::round((size_t)m) + 2 * Staging::round(96) +
+                               Staging::round(16) * 3 + Staging::round((size_t)m * 4), ctx->stream, &st)))
+        return rc;
+    if ((rc = scratch(ctx, 6, (size_t)mm * 32, &dn)) ||
         (rc = scratch(ctx, 8, 90 * 8, &dE)) || (rc = scratch(ctx, 9, 16, &dinfo)) ||
         (rc = scratch(ctx, 11, 12 * 8, &dRt)) || (rc = scratch(ctx, 12, 8, &dgood)) ||
         (rc = scratch(ctx, 13, 8, &dpick)) || (rc = scratch(ctx, 14, (size_t)mm * 4, &dpm)))
         return rc;
-    if (mask_in) {
-        if ((rc = scratch(ctx, 15, (size_t)mm, &dmin))) return rc;
-        if (m) HIP_TRY(hipMemcpy(dmin, mask_in, (size_t)m, hipMemcpyHostToDevice));
-    }
+    if (mask_in && (rc = scratch(ctx, 15, (size_t)mm, &dmin))) return rc;
+    void *dpP, *dpc;
+    if ((rc = scratch(ctx, 25, 72 * sizeof(double), &dpP)) || (rc = scratch(ctx, 26, 5 * sizeof(int32_t), &dpc)) ||
+        (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
+        return rc;
+    if (mask_in) HIP_TRY(st.put(dmin, mask_in, (size_t)m));
     const int info[4] = {3, 0, 0, DVO_OK};
-    HIP_TRY(hipMemcpy(dE, E, 9 * sizeof(double), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dinfo, info, sizeof(info), hipMemcpyHostToDevice));
+    HIP_TRY(st.put(dE, E, 9 * sizeof(double)));
+    HIP_TRY(st.put(dinfo, info, sizeof(info)));
     GeomArgs g{};
     g.pts_d = (const double*)dpts;
     g.m_const = m;
@@ -1140,25 +1237,22 @@ int dvo_recover_pose(dvo_ctx* ctx, const double* E, int e_rows, const double* p1
     g.good = (int32_t*)dgood;
     g.pick = (int32_t*)dpick;
     g.pose_mask = (uint8_t*)dpm;
-    void *dpP, *dpc;
-    if ((rc = scratch(ctx, 25, 72 * sizeof(double), &dpP)) || (rc = scratch(ctx, 26, 5 * sizeof(int32_t), &dpc))) return rc;
     g.pose_P = (double*)dpP;
     g.pose_cnt = (int32_t*)dpc;
     HIP_TRY(launch_geometry_args(g, 1, kStageNormalize | kStagePose, ctx->stream));
-    double Rt[12];
-    int gd = 0, pick = 0;
-    HIP_TRY(hipMemcpyAsync(Rt, dRt, sizeof(Rt), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(&gd, dgood, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(&pick, dpick, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    uint8_t *hRt, *hgood, *hpick, *hpm = nullptr;
+    HIP_TRY(st.get(dRt, 12 * sizeof(double), &hRt));
+    HIP_TRY(st.get(dgood, sizeof(int), &hgood));
+    HIP_TRY(st.get(dpick, sizeof(int), &hpick));
+    if (mask_out && m > 0) HIP_TRY(st.get(dpm, (size_t)m * 4, &hpm));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    std::memcpy(R, Rt, 9 * sizeof(double));
-    std::memcpy(t, Rt + 9, 3 * sizeof(double));
-    *good = gd;
-    if (mask_out && m > 0) {
-        std::vector<uint8_t> pm((size_t)m * 4);
-        HIP_TRY(hipMemcpy(pm.data(), dpm, pm.size(), hipMemcpyDeviceToHost));
-        for (int i = 0; i < m; ++i) mask_out[i] = pm[(size_t)i * 4 + pick];
-    }
+    std::memcpy(R, hRt, 9 * sizeof(double));
+    std::memcpy(t, hRt + 9 * sizeof(double), 3 * sizeof(double));
+    int pick = 0;
+    std::memcpy(good, hgood, sizeof(int));
+    std::memcpy(&pick, hpick, sizeof(int));
+    if (hpm)
+        for (int i = 0; i < m; ++i) mask_out[i] = hpm[(size_t)i * 4 + pick];
     return DVO_OK;
 }
 
@@ -1172,15 +1266,21 @@ int dvo_triangulate_points(dvo_ctx* ctx, const double* P1, const double* P2, con
     if ((rc = scratch(ctx, 16, 24 * 8, &dP)) || (rc = scratch(ctx, 17, (size_t)k * 32, &dx)) ||
         (rc = scratch(ctx, 18, (size_t)k * 32, &dX)))
         return rc;
-    double P[24];
-    std::memcpy(P, P1, 12 * sizeof(double));
-    std::memcpy(P + 12, P2, 12 * sizeof(double));
-    HIP_TRY(hipMemcpy(dP, P, sizeof(P), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(dx, x1, (size_t)k * 16, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy((char*)dx + (size_t)k * 16, x2, (size_t)k * 16, hipMemcpyHostToDevice));
+    Staging st;
+    if ((rc = staging(ctx, Staging::round(24 * 8) + Staging::round((size_t)k * 32) * 2, ctx->stream, &st))) return rc;
+    uint8_t* hP = st.take(24 * 8);
+    std::memcpy(hP, P1, 12 * sizeof(double));
+    std::memcpy(hP + 12 * sizeof(double), P2, 12 * sizeof(double));
+    HIP_TRY(st.send(dP, hP, 24 * 8));
+    uint8_t* hx = st.take((size_t)k * 32);
+    std::memcpy(hx, x1, (size_t)k * 16);
+    std::memcpy(hx + (size_t)k * 16, x2, (size_t)k * 16);
+    HIP_TRY(st.send(dx, hx, (size_t)k * 32));
     HIP_TRY(launch_triangulate((const double*)dP, (const double*)dx, k, (double*)dX, ctx->stream));
+    uint8_t* hX;
+    HIP_TRY(st.get(dX, (size_t)k * 32, &hX));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipMemcpy(X, dX, (size_t)k * 32, hipMemcpyDeviceToHost));
+    std::memcpy(X, hX, (size_t)k * 32);
     return DVO_OK;
 }
 
