@@ -148,8 +148,15 @@ constexpr int kRsW = 96, kRsLRows = 44;  // 32 * 1.25 + 2 source rows, padded to
 // Neighbouring tiles / strips share the 128-B lines of their halo columns
 // through that XCD's L2 instead of each XCD fetching its own copy.
 // Grid: nitems * xcd_frames(F) blocks; blocks past the last frame return.
-__host__ __device__ constexpr int xcd_frames(int F) { return (F + 7) & ~7; }
-__device__ __forceinline__ int xcd_frame_item(int nitems, int& item) {
+// Batches of fewer than 8 frames (the per-call surface: one frame) keep the plain
+// frame-major order, or all of a frame's blocks would land on one XCD.
+__host__ __device__ constexpr int xcd_frames(int F) { return F < 8 ? F : (F + 7) & ~7; }
+__device__ __forceinline__ int xcd_frame_item(int nitems, int nframes, int& item) {
+    if (nframes < 8) {
+        const int f = blockIdx.x / nitems;
+        item = blockIdx.x - f * nitems;
+        return f;
+    }
     const int q8 = blockIdx.x >> 3, fq = q8 / nitems;
     item = q8 - fq * nitems;
     return (blockIdx.x & 7) + 8 * fq;
@@ -158,7 +165,7 @@ __device__ __forceinline__ int xcd_frame_item(int nitems, int& item) {
 __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l, int gx) {
     __shared__ uint32_t tile[kRsLRows][kRsW];
     int item;
-    const int f = xcd_frame_item(gx * ((P.plan.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)), item);
+    const int f = xcd_frame_item(gx * ((P.plan.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)), P.nframes, item);
     if (f >= P.nframes) return;
     const int by = item / gx, bxi = item - by * gx;
     const LevelGeom& S = P.plan.L[l - 1];
@@ -364,7 +371,7 @@ __device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int s
 
 __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
     int item;
-    const int f = xcd_frame_item(P.plan.total_tiles, item);
+    const int f = xcd_frame_item(P.plan.total_tiles, P.nframes, item);
     if (f >= P.nframes) return;
     int l = 0;
     while (l + 1 < P.plan.nlevels && item >= P.plan.L[l + 1].tile_base) ++l;
@@ -405,6 +412,12 @@ __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
 // ------------------------------------------------------------------------
 // FAST-9/16 over one band of kBandRows output rows.
 constexpr int kFastNT = 256;
+#ifndef DVO_FAST_SEG_CALL
+#define DVO_FAST_SEG_CALL 8
+#endif
+// workgroups per strip: batches of fewer than 8 frames are latency-bound on the strip walk.
+// Drop-in pairs/s at 1280x720 (tools/ab_dropin.sh): 1 segment 512, 2: 523, 4: 529, 8: 533.
+__host__ __device__ constexpr int kFastSeg(int F) { return F < 8 ? DVO_FAST_SEG_CALL : 1; }
 
 __device__ __forceinline__ int fast_score16(const int* c, int v, int threshold) {
     // fast.cpp cornerScore<16> (scalar form): d[k] = v - circle[k], k in [0, 25)
@@ -542,14 +555,20 @@ __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int 
     return list[s * kSeg + e];
 }
 
-__global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
-    int strip;
-    const int f = xcd_frame_item(P.plan.total_strips, strip);
+__global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P, int nseg) {
+    // nseg > 1 (batches of a few frames): a strip's tiles are walked by nseg workgroups,
+    // segment k from tile k * ceil(nbands / nseg), each starting like tile 0 (2 more score rows)
+    int it;
+    const int f = xcd_frame_item(P.plan.total_strips * nseg, P.nframes, it);
     if (f >= P.nframes) return;
+    const int strip = it / nseg, seg = it - strip * nseg;
     int l = 0;
     while (l + 1 < P.plan.nlevels && strip >= P.plan.L[l + 1].strip_base) ++l;
     const LevelGeom& G = P.plan.L[l];
     const int c = strip - G.strip_base;
+    const int per_seg = (G.nbands + nseg - 1) / nseg;
+    const int b_begin = seg * per_seg, b_end = min(G.nbands, b_begin + per_seg);
+    if (b_begin >= b_end) return;
     const int w = G.w, h = G.h;
     const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
     const int bx = xs - 7;  // image column of LDS column 0 (a multiple of 4: kBorder - 7 and kFastTW are)
@@ -579,7 +598,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
     // per-lane offset: the rows of one wave's words differ (a scalar offset would be a waterfall).
     uint32_t creg[kFtCarryR], pf[kFtPf], screg = 0;
     {  // prologue: rows [r0-4, r0+4) into the carry registers, [r0+4, r0+kBandRows+4) into the prefetch registers
-        const int ylo = kBorder - 4;
+        const int ylo = kBorder + b_begin * kBandRows - 4;
 #pragma unroll
         for (int k = 0; k < kFtCarryR; ++k) {
             const int q = threadIdx.x + k * kFastNT;
@@ -594,8 +613,8 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         }
     }
     if (threadIdx.x == 0) ncarry[0] = 0;
-    for (int b = 0; b < G.nbands; ++b) {
-        const int par = b & 1;
+    for (int b = b_begin; b < b_end; ++b) {
+        const int par = (b - b_begin) & 1;
         const int r0 = kBorder + b * kBandRows;
         const int r1 = min(r0 + kBandRows, h - kBorder);
         const int nrows = r1 - r0;
@@ -611,14 +630,14 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
             const int q = threadIdx.x + k * kFastNT;
             if (q < kFtNewW) reinterpret_cast<uint32_t*>(img)[kFtCarryW + q] = pf[k];
         }
-        if (threadIdx.x < 2 * kFtWords) reinterpret_cast<uint32_t*>(sc)[threadIdx.x] = b == 0 ? 0u : screg;
+        if (threadIdx.x < 2 * kFtWords) reinterpret_cast<uint32_t*>(sc)[threadIdx.x] = b == b_begin ? 0u : screg;
         for (int q = threadIdx.x; q < kBandRows * kFtLW / 16; q += kFastNT)
             reinterpret_cast<uint4*>(sc + 2 * kFtLW)[q] = make_uint4(0, 0, 0, 0);
         if (threadIdx.x < kBandRows * 4) keep[threadIdx.x >> 2][threadIdx.x & 3] = 0;
         if (threadIdx.x == 0) ncarry[par ^ 1] = 0;
         __syncthreads();
         // ---- next tile: carried rows from LDS, new rows from HBM (in flight during this tile)
-        if (b + 1 < G.nbands) {
+        if (b + 1 < b_end) {
 #pragma unroll
             for (int k = 0; k < kFtCarryR; ++k) {
                 const int q = threadIdx.x + k * kFastNT;
@@ -636,7 +655,7 @@ __global__ __launch_bounds__(kFastNT) void fast_strip_kernel(StreamParams P) {
         // ---- compass, four score pixels per lane: lane -> LDS word 1 + (lane & 31) of score row
         // sr_lo + 2 (wid + 4 t) + (lane >> 5), t = 0, 1, ...
         const int nsr = nrows + 2;
-        const int sr_lo = b == 0 ? 0 : 2;
+        const int sr_lo = b == b_begin ? 0 : 2;
         {
             const int seg_off = wid * kFtSegCand, spare_i = 4 * kFtSegCand + wid * 64 + lane;
             int n = 0;  // wave-uniform
@@ -1218,9 +1237,8 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     // in turn, so one frame's keypoint windows meet in one L2 (and its
     // descriptors are written there for the matcher): 61.9-62.7 K -> 64.3 K frames/s
     const int nbx = (P.plan.kp_cap + kDKB - 1) / kDKB;
-    const int q8 = blockIdx.x >> 3, fq = q8 / nbx;
-    const int f = (blockIdx.x & 7) + 8 * fq;
-    const int bxi = q8 - fq * nbx;
+    int bxi;
+    const int f = xcd_frame_item(nbx, P.nframes, bxi);
     if (f >= P.nframes) return;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int32_t* c2 = P.buf.cnt2 + f * kMaxLevels;
@@ -1418,7 +1436,8 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
 
     mark(ev, 2, 0, s);
     if (pl.total_strips > 0)
-        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * xcd_frames(F)), dim3(kFastNT), 0, s, P);
+        hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * kFastSeg(F) * xcd_frames(F)), dim3(kFastNT), 0,
+                           s, P, kFastSeg(F));
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     if (F <= kSelCallFrames)
@@ -1432,7 +1451,7 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
         hipLaunchKernelGGL(select_harris_kernel<kSelNT>, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
-    hipLaunchKernelGGL(describe_kernel, dim3(((F + 7) / 8) * 8 * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(describe_kernel, dim3(xcd_frames(F) * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
     mark(ev, 4, 1, s);
     return hipGetLastError();
 }
