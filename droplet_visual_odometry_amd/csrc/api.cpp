@@ -371,8 +371,8 @@ int stream_alloc(dvo_stream* s) {
     A(b.gscr, (size_t)F * ((hc + 63) / 64) * 200 * 64);
     A(b.fprec, (size_t)F * ((hc + 63) / 64) * 128 * 64);
     A(b.dk_off, (size_t)F + 1);
-    A(b.dk_ctl, (size_t)4);
-    A(b.dk_list, (size_t)2 * F * hc);
+    A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
+    A(b.dk_list, (size_t)(kDkMaxPasses - 1) * F * hc);
     A(b.status, (size_t)F);
     A(b.E, (size_t)F * 90);
     A(b.info, (size_t)F * 4);
@@ -1147,7 +1147,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 20, ((hc + 63) / 64) * 200 * 64 * 8, &dgs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
-        (rc = scratch(ctx, 23, 16, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
+        (rc = scratch(ctx, 23, 4 * (2 + kDkMaxPasses), &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
         (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
         return rc;
     GeomArgs g{};

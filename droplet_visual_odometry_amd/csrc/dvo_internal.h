@@ -87,6 +87,7 @@ struct RansacState {
     int32_t best_h, best_i;  // best model: hypothesis, root
     int32_t pad[2];
 };
+constexpr int kDkMaxPasses = 4;  // Durand-Kerner passes per round (geometry.hip kDkBudgets)
 // RANSAC rounds: round r solves hypotheses [bound[r-1], min(bound[r], niters)).
 #ifndef DVO_RANSAC_BOUNDS
 #define DVO_RANSAC_BOUNDS 64, 1 << 30
@@ -125,8 +126,8 @@ struct Buffers {
     double* gscr;         // [F][ceil(hyp_cap / 64)][200][64]
     double* fprec;        // [F][ceil(hyp_cap / 64)][128][64]
     int32_t* dk_off;      // [F + 1]
-    int32_t* dk_ctl;      // [4]
-    int32_t* dk_list;     // [2][F * hyp_cap] parked Durand-Kerner polynomials
+    int32_t* dk_ctl;      // [2 + kDkMaxPasses]
+    int32_t* dk_list;     // [kDkMaxPasses - 1][F * hyp_cap] parked Durand-Kerner polynomials
     int32_t* status;      // [F] per-frame error flags
     double* E;            // [F][90]
     int32_t* info;        // [F][4] rows, inliers, iters, status
@@ -183,8 +184,8 @@ struct GeomArgs {
     double* gscr;           // [pairs][ceil(hyp_cap / 64)][200][64] five-point scratch
     double* fprec;          // [pairs][ceil(hyp_cap / 64)][128][64] five-point records
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
-    int32_t* dk_ctl;        // [4] -, pass-0 items, parked after pass 0, parked after pass 1
-    int32_t* dk_list;       // [2][dk_list_cap] parked polynomials (work-list items)
+    int32_t* dk_ctl;        // [2 + kDkMaxPasses] -, pass-0 items, parked after pass k
+    int32_t* dk_list;       // [kDkMaxPasses - 1][dk_list_cap] parked polynomials (work-list items)
     int64_t dk_list_cap;    // >= pairs * hyp_cap
     int hyp_cap;            // max(max_iters, 1)
     double* E;              // [pairs][90]

@@ -911,7 +911,21 @@ __device__ __forceinline__ int five_point(const double (&q)[5][4], double* model
     return fp_stage_c(R, models);
 }
 
-__device__ __forceinline__ float sampson_err(const double* E, double x1, double y1, double x2, double y2) {
+// EMEstimatorCallback::computeError (five-point.cpp): err = (float)(num / den)
+// with num = (x2' E x1)^2 and den = the four squared epipolar terms; the
+// inlier test err <= t (ptsetreg.cpp findInliers), decided without the f64
+// division for all but a sliver of points.  With nf = fl32(num),
+// df = fl32(den), s = fl32(t * df) (relative errors <= 2^-24 each while the
+// values are normal floats, which the range checks on t and s guarantee):
+//   nf < fl32(s * (1 - 2^-20))  =>  num < t * den  =>  fl64(num / den) <= t (RN is
+//                                   monotone and t is a double), so (float) <= t;
+//   nf > fl32(s * (1 + 2^-20))  =>  num / den > t (1 + 2^-21)  =>  the double
+//                                   quotient is past t's rounding midpoint
+//                                   (half an ulp <= t 2^-24), so (float) > t.
+// (nf zero, denormal or +inf only strengthens either inequality.)  Otherwise,
+// and for NaN, the exact division decides.  Bit-identical inlier sets.
+__device__ __forceinline__ bool sampson_inlier(const double* E, double x1, double y1, double x2, double y2, float t,
+                                               bool fast_ok) {
     double ex0 = E[0] * x1 + E[1] * y1 + E[2] * 1.;
     double ex1 = E[3] * x1 + E[4] * y1 + E[5] * 1.;
     double ex2 = E[6] * x1 + E[7] * y1 + E[8] * 1.;
@@ -919,7 +933,15 @@ __device__ __forceinline__ float sampson_err(const double* E, double x1, double 
     double et1 = E[1] * x2 + E[4] * y2 + E[7] * 1.;
     double x2tEx1 = x2 * ex0 + y2 * ex1 + 1. * ex2;
     double a = ex0 * ex0, b = ex1 * ex1, c = et0 * et0, d = et1 * et1;
-    return (float)(x2tEx1 * x2tEx1 / (a + b + c + d));
+    const double num = x2tEx1 * x2tEx1, den = a + b + c + d;
+    if (fast_ok) {
+        const float nf = (float)num, s = t * (float)den;
+        if (s >= 1e-30f && s <= 1e30f) {
+            if (nf < s * (1.f - 0x1p-20f)) return true;
+            if (nf > s * (1.f + 0x1p-20f)) return false;
+        }
+    }
+    return (float)(num / den) <= t;
 }
 
 __device__ int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
@@ -980,7 +1002,10 @@ constexpr int kSolveNT = 64;
 #ifndef DVO_SCORE_CHUNK
 #define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
 #endif
-constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
+#ifndef DVO_SCORE_MB
+#define DVO_SCORE_MB 1  // models per wave pass over a chunk's points; measured (two-stream bench): 1 73.0 K, 2 72.6 K, 4 71.4 K frames/s
+#endif
+constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK, kScoreMB = DVO_SCORE_MB;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
 // one wave per pair: idx[i] = rng.uniform(0, m) = rng.next() % m, redrawn
@@ -1187,8 +1212,7 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
         g.dk_off[pairs] = s_carry;
         g.dk_ctl[0] = 0;
         g.dk_ctl[1] = s_carry;  // pass 0 items
-        g.dk_ctl[2] = 0;        // parked after pass 0
-        g.dk_ctl[3] = 0;        // parked after pass 1
+        for (int k = 0; k < kDkMaxPasses; ++k) g.dk_ctl[2 + k] = 0;  // parked after pass k
     }
 }
 
@@ -1225,7 +1249,20 @@ __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
 // keeps every wave of the round resident (it needed all of them for ~300
 // sweeps before).
 constexpr int kDkNT = 256;
-constexpr int kDkBudget0 = 48, kDkBudget1 = 80;  // sweeps of passes 0 and 1; pass 2 runs to the end
+// Sweeps of each pass but the last, which runs to the end; a zero ends the list.
+// Between passes the unfinished polynomials are compacted, so the waves of the
+// next pass are full.
+#ifndef DVO_DK_B0
+#define DVO_DK_B0 48
+#endif
+#ifndef DVO_DK_B1
+#define DVO_DK_B1 80
+#endif
+#ifndef DVO_DK_B2
+#define DVO_DK_B2 0
+#endif
+constexpr int kDkBudgets[kDkMaxPasses - 1] = {DVO_DK_B0, DVO_DK_B1, DVO_DK_B2};
+constexpr int kDkPasses = DVO_DK_B0 == 0 ? 1 : DVO_DK_B1 == 0 ? 2 : DVO_DK_B2 == 0 ? 3 : 4;
 constexpr int kRecSnap = 108;                     // parked: Brent snapshot (20 doubles)
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
@@ -1453,23 +1490,33 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     for (int e = tid; e < T; e += kScoreNT) s_cnt[e] = 0;
     const double thr = g.threshold / ((g.fx + g.fy) / 2);
     const float t = (float)(thr * thr);
+    const bool fast_ok = t >= FLT_MIN;  // the division-free test needs t normal
     const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
     for (int c0 = 0; c0 < m; c0 += kScoreChunk) {
         const int cn = min(kScoreChunk, m - c0);
         __syncthreads();
         for (int e = tid; e < cn * 4; e += kScoreNT) s_pts[e] = npts[(int64_t)c0 * 4 + e];
         __syncthreads();
-        for (int e = wid; e < T; e += kScoreNT / 64) {
-            double Ed[9];
+        // kScoreMB models per wave at a time: each point is read from LDS once for all of them
+        for (int e0 = wid * kScoreMB; e0 < T; e0 += kScoreNT / 64 * kScoreMB) {
+            double Ed[kScoreMB][9];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
-            int cnt = 0;
+            for (int q = 0; q < kScoreMB; ++q)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Ed[q][k] = s_E[min(e0 + q, T - 1) * 9 + k];
+            int cnt[kScoreMB] = {};
             for (int j = lane; j < cn; j += 64) {
                 const double* pt = s_pts + j * 4;
-                const float err = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]);
-                cnt += __popcll(__ballot(err <= t));
+                const double x1 = pt[0], y1 = pt[1], x2 = pt[2], y2 = pt[3];
+#pragma unroll
+                for (int q = 0; q < kScoreMB; ++q)
+                    cnt[q] += __popcll(__ballot(sampson_inlier(Ed[q], x1, y1, x2, y2, t, fast_ok)));
             }
-            if (lane == 0) s_cnt[e] += cnt;
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < kScoreMB; ++q)
+                    if (e0 + q < T) s_cnt[e0 + q] += cnt[q];
+            }
         }
     }
     __syncthreads();
@@ -1645,7 +1692,7 @@ __global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
         const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
         for (int j = threadIdx.x; j < m; j += 256) {
             const double* pt = npts + (int64_t)j * 4;
-            g.mask[(int64_t)p * g.pts_stride + j] = sampson_err(Ed, pt[0], pt[1], pt[2], pt[3]) <= t;
+            g.mask[(int64_t)p * g.pts_stride + j] = sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, t >= FLT_MIN);
         }
     }
 }
@@ -1671,9 +1718,9 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) 
                                pairs);
         } else {
             const dim3 dgrid((unsigned)(((int64_t)pairs * span + kDkNT - 1) / kDkNT));
-            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 0, kDkBudget0);
-            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 1, kDkBudget1);
-            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, 2, 1 << 30);
+            for (int pass = 0; pass < kDkPasses; ++pass)
+                hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
+                                   pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
         }
         hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
         hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
