@@ -1350,21 +1350,22 @@ __device__ __forceinline__ double row_bcast(double v) {
     return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// Only lane T's own work sits inside the masked block: its old-root factors
+// d[j] = z_T - z_j (j > T, still old at step T) are formed by every lane at the
+// start of the sweep, and the moved / zero tests run once after the sweep.
 template <int T>
-__device__ __forceinline__ void dkw_step(const Cx& num, Cx& den, Cx& mine, Cx (&roots)[10], int r, bool& moved_l,
-                                         bool& zero_l) {
+__device__ __forceinline__ void dkw_step(const Cx& num, Cx& den, Cx& mine, Cx (&roots)[10], const Cx (&d)[10], int r,
+                                         Cx& q) {
     if constexpr (T < 10) {
         if (r == T) {
 #pragma unroll
-            for (int j = T + 1; j < 10; ++j) den = cmul(den, csub(mine, roots[j]));
-            zero_l = !(den.re != 0 || den.im != 0) || den.re != den.re || den.im != den.im;
-            const Cx q = cdiv(num, den);
+            for (int j = T + 1; j < 10; ++j) den = cmul(den, d[j]);
+            q = cdiv(num, den);
             mine = csub(mine, q);
-            moved_l = (q.re * q.re + q.im * q.im) > 0;
         }
         roots[T] = Cx{row_bcast<T>(mine.re), row_bcast<T>(mine.im)};
         if (r > T) den = cmul(den, csub(mine, roots[T]));
-        dkw_step<T + 1>(num, den, mine, roots, r, moved_l, zero_l);
+        dkw_step<T + 1>(num, den, mine, roots, d, r, q);
     }
 }
 
@@ -1406,9 +1407,14 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
             const Cx t = cmul(num, mine);
             num = Cx{t.re + c[10 - j - 1], t.im + 0.0};
         }
-        Cx den{c[10], 0};
-        bool moved_l = false, zero_l = false;
-        dkw_step<0>(num, den, mine, roots, r, moved_l, zero_l);
+        Cx d[10];
+#pragma unroll
+        for (int j = 0; j < 10; j++) d[j] = csub(mine, roots[j]);
+        Cx den{c[10], 0}, q{0, 0};
+        dkw_step<0>(num, den, mine, roots, d, r, q);
+        // lane r's den is final after its own step (later steps only touch lanes r > T)
+        const bool zero_l = !(den.re != 0 || den.im != 0) || den.re != den.re || den.im != den.im;
+        const bool moved_l = (q.re * q.re + q.im * q.im) > 0;
         const bool moved = (__ballot(moved_l && r < 10) & own) != 0;
         const bool same = (__ballot(zero_l && r < 10) & own) != 0;
         const bool eq_l = __builtin_bit_cast(long long, mine.re) == __builtin_bit_cast(long long, saved.re) &&
