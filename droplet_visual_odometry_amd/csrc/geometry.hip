@@ -825,26 +825,68 @@ __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, 
 // Stage C: roots -> (x, y, z) by the 3x3 null space of B(z) -> E, normalised.
 // Polynomials flagged generic (leading coefficient negligible) are solved here.
 __device__ __forceinline__ void dk_store(double* R, Cx (&roots)[10]);
-__device__ __forceinline__ int fp_stage_c(double* R, double* models) {
+// The model of one real root z1 (five-point.cpp getModels, per root): x, y from
+// the SVD of the 3x3 B(z1), E = x X + y Y + z W + Z normalised.  False when the
+// root is rejected (|v22| < 1e-10).
+__device__ __forceinline__ bool root_model(const double (&b)[39], const double (&EE)[36], double z1, double (&out)[9]) {
+    double z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
+    double bz[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const double* br = b + j * 13;
+        bz[j][0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
+        bz[j][1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
+        bz[j][2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
+    }
+    double at3[3][3], w3[3], vt3[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) at3[r][k] = bz[k][r];
+    jacobi_svd<3, 3, 0, 3>(at3, w3, vt3);
+    if (fabs(vt3[2][2]) < 1e-10) return false;
+    double xs = vt3[2][0] / vt3[2][2], ys = vt3[2][1] / vt3[2][2];
+    double e[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) e[k] = (((EE[k] * xs + EE[9 + k] * ys) + 0.0) + EE[18 + k] * z1) + EE[27 + k];
+    double s = 0;
+    s += e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3];
+    s += e[4] * e[4] + e[5] * e[5] + e[6] * e[6] + e[7] * e[7];
+    s += e[8] * e[8];
+    double inv_n = 1. / sqrt(s);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[k] = e[k] * inv_n + 0.0;
+    return true;
+}
+
+// Roots of a polynomial stage A flagged for an exact solve (2: coincident roots
+// in Durand-Kerner, other nonzero: the generic solver), stored in the record.
+__device__ __forceinline__ void fp_exact_roots(double* R, bool store) {
     if (R[kRecGeneric * 64] == 2.0) {
         double c[11];
         Cx roots[10];
 #pragma unroll
         for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
         solve_poly10(c, roots);
-        dk_store(R, roots);
+        if (store) dk_store(R, roots);
     } else if (R[kRecGeneric * 64] != 0.0) {
         double c[11];
         Cx roots[10];
 #pragma unroll
         for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
         const int nr = solve_poly_generic(c, 10, roots);
-        for (int i = 0; i < nr; ++i) {
-            R[(kRecRoots + 2 * i) * 64] = roots[i].re;
-            R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
+        if (store) {
+            for (int i = 0; i < nr; ++i) {
+                R[(kRecRoots + 2 * i) * 64] = roots[i].re;
+                R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
+            }
+            R[kRecNr * 64] = nr;
         }
-        R[kRecNr * 64] = nr;
     }
+}
+
+__device__ __forceinline__ int fp_stage_c(double* R, double* models) {
+    fp_exact_roots(R, true);
     double b[39], EE[36];
 #pragma unroll
     for (int k = 0; k < 39; ++k) b[k] = R[(kRecB + k) * 64];
@@ -854,34 +896,11 @@ __device__ __forceinline__ int fp_stage_c(double* R, double* models) {
     int count = 0;
     for (int i = 0; i < nr; ++i) {
         if (fabs(R[(kRecRoots + 2 * i + 1) * 64]) > 1e-10) continue;
-        double z1 = R[(kRecRoots + 2 * i) * 64], z2 = z1 * z1, z3 = z2 * z1, z4 = z3 * z1;
-        double bz[3][3];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const double* br = b + j * 13;
-            bz[j][0] = br[0] * z3 + br[1] * z2 + br[2] * z1 + br[3];
-            bz[j][1] = br[4] * z3 + br[5] * z2 + br[6] * z1 + br[7];
-            bz[j][2] = br[8] * z4 + br[9] * z3 + br[10] * z2 + br[11] * z1 + br[12];
-        }
-        double at3[3][3], w3[3], vt3[3][3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) at3[r][k] = bz[k][r];
-        jacobi_svd<3, 3, 0, 3>(at3, w3, vt3);
-        if (fabs(vt3[2][2]) < 1e-10) continue;
-        double xs = vt3[2][0] / vt3[2][2], ys = vt3[2][1] / vt3[2][2];
         double e[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) e[k] = (((EE[k] * xs + EE[9 + k] * ys) + 0.0) + EE[18 + k] * z1) + EE[27 + k];
-        double s = 0;
-        s += e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3];
-        s += e[4] * e[4] + e[5] * e[5] + e[6] * e[6] + e[7] * e[7];
-        s += e[8] * e[8];
-        double inv_n = 1. / sqrt(s);
+        if (!root_model(b, EE, R[(kRecRoots + 2 * i) * 64], e)) continue;
         double* out = models + count * 9;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) out[k] = e[k] * inv_n + 0.0;
+        for (int k = 0; k < 9; ++k) out[k] = e[k];
         count++;
     }
     return count;
@@ -1462,6 +1481,72 @@ __global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
         fp_stage_c(hyp_record(g, p, h), g.models + ((int64_t)p * g.hyp_cap + h) * 90);
 }
 
+// Stage C for rounds with few hypotheses (the per-call findEssentialMat): one
+// 16-lane row per hypothesis, lane i builds the model of root i, so a
+// hypothesis costs one 3x3 SVD of latency instead of one per real root.  The
+// models keep the root order of fp_stage_c (a ballot prefix over the row).
+__global__ __launch_bounds__(64) void ransac_stage_c_row_kernel(GeomArgs g) {
+    const int p = blockIdx.y;
+    const RansacState& S = g.rs[p];
+    const int lane = threadIdx.x, r = lane & 15, rowbase = lane & ~15;
+    const int h = S.h0 + blockIdx.x * 4 + (lane >> 4);
+    const bool act = h < S.h1;
+    double* R = act ? hyp_record(g, p, h) : nullptr;
+    int nr = 0;
+    double zre = 0, zim = 0;
+    if (act) {
+        const double gen = R[kRecGeneric * 64];
+        if (gen == 0.0) {
+            nr = (int)R[kRecNr * 64];
+            if (r < nr) {
+                zre = R[(kRecRoots + 2 * r) * 64];
+                zim = R[(kRecRoots + 2 * r + 1) * 64];
+            }
+        } else {  // every lane of the row solves (same inputs, same roots); lane 0 records them
+            double c[11];
+            Cx roots[10];
+#pragma unroll
+            for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
+            if (gen == 2.0) {
+                solve_poly10(c, roots);
+                dk_finish(roots);
+                nr = 10;
+            } else {
+                nr = solve_poly_generic(c, 10, roots);
+            }
+            for (int i = 0; i < nr; ++i)
+                if (i == r) {
+                    zre = roots[i].re;
+                    zim = roots[i].im;
+                }
+            if (r == 0) {
+                for (int i = 0; i < nr; ++i) {
+                    R[(kRecRoots + 2 * i) * 64] = roots[i].re;
+                    R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
+                }
+                R[kRecNr * 64] = nr;
+            }
+        }
+    }
+    bool valid = false;
+    double e[9];
+    if (act && r < nr && !(fabs(zim) > 1e-10)) {
+        double b[39], EE[36];
+#pragma unroll
+        for (int k = 0; k < 39; ++k) b[k] = R[(kRecB + k) * 64];
+#pragma unroll
+        for (int k = 0; k < 36; ++k) EE[k] = R[(kRecEE + k) * 64];
+        valid = root_model(b, EE, zre, e);
+    }
+    const uint32_t rowbits = (uint32_t)(__ballot(valid) >> rowbase) & 0xFFFFu;
+    if (valid) {
+        double* out = g.models + ((int64_t)p * g.hyp_cap + h) * 90 + __popc(rowbits & ((1u << r) - 1u)) * 9;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) out[k] = e[k];
+    }
+    if (act && r == 0) g.nmod[(int64_t)p * g.hyp_cap + h] = __popc(rowbits);
+}
+
 // Inlier counts of every root of kScoreHyps hypotheses of one pair; the pair's
 // normalised points stream through LDS in chunks, one wave per model.
 __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
@@ -1728,7 +1813,10 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) 
                 hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
                                    pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
         }
-        hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
+        if (one)
+            hipLaunchKernelGGL(ransac_stage_c_row_kernel, dim3((span + 3) / 4, pairs), dim3(64), 0, s, g);
+        else
+            hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
         hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
                            s, g);
         hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
