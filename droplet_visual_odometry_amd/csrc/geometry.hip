@@ -1024,7 +1024,11 @@ constexpr int kSolveNT = 64;
 #ifndef DVO_SCORE_MB
 #define DVO_SCORE_MB 1  // models per wave pass over a chunk's points; measured (two-stream bench): 1 73.0 K, 2 72.6 K, 4 71.4 K frames/s
 #endif
+#ifndef DVO_SCORE_HYPS_CALL
+#define DVO_SCORE_HYPS_CALL 2  // drop-in pairs/s (profiles/r02z_ab_dropin_score_hyps.txt): 1 620, 2 626, 4 611, 16 610
+#endif
 constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK, kScoreMB = DVO_SCORE_MB;
+constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
 // one wave per pair: idx[i] = rng.uniform(0, m) = rng.next() % m, redrawn
@@ -1547,20 +1551,23 @@ __global__ __launch_bounds__(64) void ransac_stage_c_row_kernel(GeomArgs g) {
     if (act && r == 0) g.nmod[(int64_t)p * g.hyp_cap + h] = __popc(rowbits);
 }
 
-// Inlier counts of every root of kScoreHyps hypotheses of one pair; the pair's
+// Inlier counts of every root of HYPS hypotheses of one pair; the pair's
 // normalised points stream through LDS in chunks, one wave per model.
+// HYPS = kScoreHyps for batches; the per-call path (one pair) takes kScoreHypsCall
+// so that its few blocks spread over more CUs (fewer models per wave in sequence).
+template <int HYPS>
 __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
-    const int hb = S.h0 + blockIdx.x * kScoreHyps;
+    const int hb = S.h0 + blockIdx.x * HYPS;
     if (hb >= S.h1 || S.m <= 5) return;
-    const int hn = min(kScoreHyps, S.h1 - hb);
+    const int hn = min(HYPS, S.h1 - hb);
     const int m = S.m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ double s_pts[kScoreChunk * 4];
-    __shared__ double s_E[kScoreHyps * 10 * 9];
-    __shared__ int s_pref[kScoreHyps + 1];
-    __shared__ int s_cnt[kScoreHyps * 10];
+    __shared__ double s_E[HYPS * 10 * 9];
+    __shared__ int s_pref[HYPS + 1];
+    __shared__ int s_cnt[HYPS * 10];
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
     if (tid == 0) {
         int acc = 0;
@@ -1817,8 +1824,12 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) 
             hipLaunchKernelGGL(ransac_stage_c_row_kernel, dim3((span + 3) / 4, pairs), dim3(64), 0, s, g);
         else
             hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        hipLaunchKernelGGL(ransac_score_kernel, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs), dim3(kScoreNT), 0,
-                           s, g);
+        if (one)
+            hipLaunchKernelGGL(ransac_score_kernel<kScoreHypsCall>,
+                               dim3((span + kScoreHypsCall - 1) / kScoreHypsCall, pairs), dim3(kScoreNT), 0, s, g);
+        else
+            hipLaunchKernelGGL(ransac_score_kernel<kScoreHyps>, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs),
+                               dim3(kScoreNT), 0, s, g);
         hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
     }
     hipLaunchKernelGGL(ransac_finish_kernel, dim3(pairs), dim3(256), 0, s, g);

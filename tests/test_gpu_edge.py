@@ -141,3 +141,41 @@ def test_golden_fixture_on_gpu(gpu_ctx):
     np.testing.assert_array_equal(R, g["R"])
     np.testing.assert_array_equal(t.reshape(3, 1), g["t_unit"])
     assert good == int(g["good"])
+
+
+def _degenerate_sets():
+    rng = np.random.default_rng(7)
+    K = np.array([[500.0, 0, 320], [0, 500, 240], [0, 0, 1]])
+    X = np.c_[rng.uniform(-1, 1, (30, 2)), rng.uniform(3, 6, 30)]
+    p1 = X[:, :2] / X[:, 2:] * 500 + [320, 240]
+    X2 = X - [0.3, 0.1, 0.0]
+    p2 = X2[:, :2] / X2[:, 2:] * 500 + [320, 240]
+    line = np.c_[np.linspace(100, 500, 30), np.linspace(50, 400, 30)]
+    return {
+        "identical": (p1, p1.copy(), K),                      # no motion: every skew E fits
+        "repeated": (np.repeat(p1[:8], 4, 0), np.repeat(p2[:8], 4, 0), K),  # 8 distinct pairs, 4 copies each
+        "collinear": (line, line + [3.0, 0.0], K),            # all points on one line in both views
+        "integer": (np.round(p1), np.round(p2), K),           # pixel-quantised, as ORB keypoints at level 0
+        "pure_rotation": (p1, (p1 - [320, 240]) @ np.array([[0.99, -0.14], [0.14, 0.99]]) + [320, 240], K),
+    }
+
+
+@pytest.mark.parametrize("case", ["identical", "repeated", "collinear", "integer", "pure_rotation"])
+def test_degenerate_correspondences(gpu_ctx, oracle_mod, case):
+    """Degenerate point sets drive the 5-point solver into its rare branches
+    (vanishing polynomial coefficients, coincident Durand-Kerner roots, rejected
+    roots); the per-call findEssentialMat (one-round RANSAC, 16-lane Durand-Kerner
+    and stage-C rows) must still agree with the oracle bit for bit."""
+    from droplet_visual_odometry_amd import ops
+    from droplet_visual_odometry_amd._native import DVOError
+    p1, p2, K = _degenerate_sets()[case]
+    p1 = np.ascontiguousarray(p1, dtype=np.float64)
+    p2 = np.ascontiguousarray(p2, dtype=np.float64)
+    Eo, mo, io = oracle_mod.find_essential(p1, p2, K)
+    if Eo is None:
+        with pytest.raises(DVOError):
+            ops.find_essential_mat(p1, p2, K, ctx=gpu_ctx)
+        return
+    E, mask = ops.find_essential_mat(p1, p2, K, ctx=gpu_ctx)
+    np.testing.assert_array_equal(E, Eo)
+    np.testing.assert_array_equal(mask.ravel(), mo.ravel())
