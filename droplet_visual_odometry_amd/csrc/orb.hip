@@ -1060,8 +1060,17 @@ constexpr int kSelNT = DVO_SEL_NT;
 #define DVO_SEL_NT_CALL 512
 #endif
 constexpr int kSelNTCall = DVO_SEL_NT_CALL, kSelCallFrames = 4;
+// The per-call kernels (one block per level, nothing else on the GPU) run the
+// selection on an LDS copy of the level's list when it fits: every partition
+// step's reads, scans and swaps are then LDS round trips instead of HBM ones.
+// Lists longer than this (very textured frames) take the global-memory path.
+constexpr int kSelLdsCap = 8192;
+#ifndef DVO_SEL_LDS_CALL
+#define DVO_SEL_LDS_CALL 1
+#endif
+constexpr bool kSelLdsCall = DVO_SEL_LDS_CALL != 0;
 
-template <int NT>
+template <int NT, bool kLds>
 __global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
     const int l = blockIdx.x, f = blockIdx.y;
     if (l >= P.plan.nlevels) return;
@@ -1098,7 +1107,22 @@ __global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
     __syncthreads();
     int32_t* Lpos = P.buf.sel_tmp + (int64_t)f * 2 * P.plan.cand_stride + 2 * G.cand_off;
     int32_t* Rasc = Lpos + G.cand_cap;
-    const int k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+    int k;
+    if constexpr (kLds) {
+        __shared__ uint32_t s_key[kSelLdsCap];
+        __shared__ int32_t s_L[kSelLdsCap], s_R[kSelLdsCap];
+        if (n <= kSelLdsCap) {
+            for (int i = threadIdx.x; i < n; i += NT) s_key[i] = A[i];
+            __syncthreads();
+            k = retain_best_block(FastKeys{s_key}, n, 2 * G.nper, -1, s_L, s_R, lds);
+            __syncthreads();
+            for (int i = threadIdx.x; i < k; i += NT) A[i] = s_key[i];
+        } else {
+            k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+        }
+    } else {
+        k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+    }
     if (threadIdx.x == 0) P.buf.cnt1[f * kMaxLevels + l] = k;
 }
 
@@ -1176,7 +1200,7 @@ __global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
     }
 }
 
-template <int NT>
+template <int NT, bool kLds>
 __global__ __launch_bounds__(NT) void select_harris_kernel(StreamParams P) {
     const int l = blockIdx.x, f = blockIdx.y;
     if (l >= P.plan.nlevels) return;
@@ -1187,7 +1211,29 @@ __global__ __launch_bounds__(NT) void select_harris_kernel(StreamParams P) {
     float* R = P.buf.resp + (int64_t)f * P.plan.cand_stride + G.cand_off;
     int32_t* Lpos = P.buf.sel_tmp + (int64_t)f * 2 * P.plan.cand_stride + 2 * G.cand_off;
     int32_t* Rasc = Lpos + G.cand_cap;
-    const int k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+    int k;
+    if constexpr (kLds) {
+        __shared__ float s_v[kSelLdsCap];
+        __shared__ uint32_t s_key[kSelLdsCap];
+        __shared__ int32_t s_L[kSelLdsCap], s_R[kSelLdsCap];
+        if (n <= kSelLdsCap) {
+            for (int i = threadIdx.x; i < n; i += NT) {
+                s_v[i] = R[i];
+                s_key[i] = A[i];
+            }
+            __syncthreads();
+            k = retain_best_block(HarrisVals{s_v, s_key}, n, G.nper, -1, s_L, s_R, lds);
+            __syncthreads();
+            for (int i = threadIdx.x; i < k; i += NT) {
+                R[i] = s_v[i];
+                A[i] = s_key[i];
+            }
+        } else {
+            k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+        }
+    } else {
+        k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+    }
     if (threadIdx.x == 0) P.buf.cnt2[f * kMaxLevels + l] = k;
 }
 
@@ -1441,14 +1487,15 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     if (F <= kSelCallFrames)
-        hipLaunchKernelGGL(select_fast_kernel<kSelNTCall>, dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
+        hipLaunchKernelGGL((select_fast_kernel<kSelNTCall, kSelLdsCall>), dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
     else
-        hipLaunchKernelGGL(select_fast_kernel<kSelNT>, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+        hipLaunchKernelGGL((select_fast_kernel<kSelNT, false>), dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     hipLaunchKernelGGL(harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
     if (F <= kSelCallFrames)
-        hipLaunchKernelGGL(select_harris_kernel<kSelNTCall>, dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
+        hipLaunchKernelGGL((select_harris_kernel<kSelNTCall, kSelLdsCall>), dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s,
+                           P);
     else
-        hipLaunchKernelGGL(select_harris_kernel<kSelNT>, dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+        hipLaunchKernelGGL((select_harris_kernel<kSelNT, false>), dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
     mark(ev, 3, 1, s);
     mark(ev, 4, 0, s);
     hipLaunchKernelGGL(describe_kernel, dim3(xcd_frames(F) * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);

@@ -179,3 +179,16 @@ def test_degenerate_correspondences(gpu_ctx, oracle_mod, case):
     E, mask = ops.find_essential_mat(p1, p2, K, ctx=gpu_ctx)
     np.testing.assert_array_equal(E, Eo)
     np.testing.assert_array_equal(mask.ravel(), mo.ravel())
+
+
+def test_detect_noise_frame_long_lists(gpu_ctx, oracle_mod):
+    """A 1280x720 noise frame: ~90 K FAST survivors at level 0 (levels 0-4 past the
+    per-call selection's LDS capacity of 8192, levels 5-7 inside it), so both the
+    LDS and the global-memory retainBest paths run in one call, bit-exact."""
+    from droplet_visual_odometry_amd import ops
+    rng = np.random.default_rng(3)
+    img = np.ascontiguousarray(rng.integers(0, 256, (720, 1280), dtype=np.uint8))
+    kg, dg = ops.detect_and_compute(img, 2000, ctx=gpu_ctx)
+    ko, do = oracle_mod.detect_and_compute(img, 2000)
+    np.testing.assert_array_equal(kg.view(np.uint8), ko.view(np.uint8))
+    np.testing.assert_array_equal(dg, do)
