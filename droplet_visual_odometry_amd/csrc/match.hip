@@ -297,42 +297,63 @@ __global__ __launch_bounds__(kXNT) void crosscheck_stream_kernel(StreamParams P,
 }
 
 // Single pair (C-ABI dvo_bf_match_hamming): output in queryIdx order like
-// OpenCV (the caller's Python applies the stable distance sort itself).
+// OpenCV's raw list (the caller's Python applies the stable distance sort), so
+// no sort is needed: the kept queries are compacted in ascending q with a
+// block-wide exclusive scan, 1024 queries per round.
 __global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* fwd, const int32_t* bwd, int nq, int nt,
                                                                int mode, dvo_dmatch* out, int* m_out) {
-    __shared__ uint32_t keys[2 * kMaxSort];
-    __shared__ int scan_lds[32];
-    const int m = crosscheck_sort(fwd, bwd, nq, nt, mode, keys, scan_lds);
-    // re-sort by queryIdx: keys are unique (d<<16|q); rewrite as (q<<16|d) and sort again
-    for (int i = threadIdx.x; i < m; i += kXNT) {
-        uint32_t k = keys[i];
-        keys[i] = ((k & 0xFFFF) << 16) | (k >> 16);
+    __shared__ uint32_t best[kMaxSort];  // mode 2: per query min (d << 16 | t) over the trains naming it
+    __shared__ int s_wave[kXNT / 64];
+    __shared__ int s_carry;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (mode == 2) {
+        // OpenCV 3.x: for each train t (reverse NN q = bwd[t]), keep per query the
+        // train with the smallest distance, first t on ties.
+        for (int q = threadIdx.x; q < nq; q += kXNT) best[q] = 0xFFFFFFFFu;
+        __syncthreads();
+        for (int t = threadIdx.x; t < nt; t += kXNT) {
+            const int b = bwd[t];
+            if (b < 0 || (b >> 16) > 256) continue;  // -1 or the untouched 0x7F7F7F7F fill
+            atomicMin(&best[b & 0xFFFF], ((uint32_t)(b >> 16) << 16) | (uint32_t)t);
+        }
     }
+    if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
-    int n2 = 1;
-    while (n2 < m) n2 <<= 1;
-    for (int k = 2; k <= n2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n2; i += kXNT) {
-                int ixj = i ^ j;
-                if (ixj > i) {
-                    uint32_t a = keys[i], b = keys[ixj];
-                    bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        keys[i] = b;
-                        keys[ixj] = a;
-                    }
+    for (int q0 = 0; q0 < nq; q0 += kXNT) {
+        const int q = q0 + threadIdx.x;
+        bool keep = false;
+        int t = 0, d = 0;
+        if (q < nq) {
+            if (mode == 2) {
+                const uint32_t k = best[q];
+                keep = k != 0xFFFFFFFFu;
+                t = (int)(k & 0xFFFF);
+                d = (int)(k >> 16);
+            } else {
+                const int f = fwd[q];
+                if (f >= 0) {
+                    t = f & 0xFFFF;
+                    d = f >> 16;
+                    keep = mode != 1 || (bwd[t] & 0xFFFF) == q;
                 }
             }
-            __syncthreads();
         }
-    for (int i = threadIdx.x; i < m; i += kXNT) {
-        const uint32_t k = keys[i];
-        const int q = k >> 16, d = k & 0xFFFF;
-        const int t = mode == 2 ? (int)(keys[kMaxSort + q] & 0xFFFF) : (fwd[q] & 0xFFFF);
-        out[i] = dvo_dmatch{q, t, 0, (float)d};
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) s_wave[wid] = __popcll(bal);
+        __syncthreads();
+        int off = s_carry, tot = 0;
+        for (int w = 0; w < kXNT / 64; ++w) {
+            const int c = s_wave[w];
+            off += w < wid ? c : 0;
+            tot += c;
+        }
+        off += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (keep) out[off] = dvo_dmatch{q, t, 0, (float)d};
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
     }
-    if (threadIdx.x == 0) *m_out = m;
+    if (threadIdx.x == 0) *m_out = s_carry;
 }
 
 }  // namespace
