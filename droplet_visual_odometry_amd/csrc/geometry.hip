@@ -1021,13 +1021,10 @@ constexpr int kSolveNT = 64;
 #ifndef DVO_SCORE_CHUNK
 #define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
 #endif
-#ifndef DVO_SCORE_MB
-#define DVO_SCORE_MB 1  // models per wave pass over a chunk's points; measured (two-stream bench): 1 73.0 K, 2 72.6 K, 4 71.4 K frames/s
-#endif
 #ifndef DVO_SCORE_HYPS_CALL
 #define DVO_SCORE_HYPS_CALL 2  // drop-in pairs/s (profiles/r02z_ab_dropin_score_hyps.txt): 1 620, 2 626, 4 611, 16 610
 #endif
-constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK, kScoreMB = DVO_SCORE_MB;
+constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
@@ -1595,26 +1592,18 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         __syncthreads();
         for (int e = tid; e < cn * 4; e += kScoreNT) s_pts[e] = npts[(int64_t)c0 * 4 + e];
         __syncthreads();
-        // kScoreMB models per wave at a time: each point is read from LDS once for all of them
-        for (int e0 = wid * kScoreMB; e0 < T; e0 += kScoreNT / 64 * kScoreMB) {
-            double Ed[kScoreMB][9];
+        // one wave per model (2 or 4 models per wave pass over the chunk, reading each point
+        // once, measured slower: 73.0 K vs 72.6 / 71.4 K frames/s, profiles/r02w_ab_score_dk.txt)
+        for (int e = wid; e < T; e += kScoreNT / 64) {
+            double Ed[9];
 #pragma unroll
-            for (int q = 0; q < kScoreMB; ++q)
-#pragma unroll
-                for (int k = 0; k < 9; ++k) Ed[q][k] = s_E[min(e0 + q, T - 1) * 9 + k];
-            int cnt[kScoreMB] = {};
+            for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
+            int cnt = 0;
             for (int j = lane; j < cn; j += 64) {
                 const double* pt = s_pts + j * 4;
-                const double x1 = pt[0], y1 = pt[1], x2 = pt[2], y2 = pt[3];
-#pragma unroll
-                for (int q = 0; q < kScoreMB; ++q)
-                    cnt[q] += __popcll(__ballot(sampson_inlier(Ed[q], x1, y1, x2, y2, t, fast_ok)));
+                cnt += __popcll(__ballot(sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok)));
             }
-            if (lane == 0) {
-#pragma unroll
-                for (int q = 0; q < kScoreMB; ++q)
-                    if (e0 + q < T) s_cnt[e0 + q] += cnt[q];
-            }
+            if (lane == 0) s_cnt[e] += cnt;
         }
     }
     __syncthreads();
