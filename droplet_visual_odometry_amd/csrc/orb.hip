@@ -1175,14 +1175,21 @@ __global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
 // is formed exactly as the scalar code does.
 // Harris grid width: sized for 2n per level (the FAST-retained list is >= 2n
 // with ties, known only on the device), grid-stride beyond that
+// kHG keypoint groups per wave: every group's window words are requested before
+// any is used, so one load latency covers kHG groups (the kernel is latency-bound:
+// one group per wave left each wave a single load round trip of work).
+#ifndef DVO_HARRIS_GROUPS
+#define DVO_HARRIS_GROUPS 2  // two-stream bench: 1 73.6 K, 2 74.7 K, 4 74.6 K frames/s (profiles/r02z_ab_harris_groups.txt)
+#endif
+constexpr int kHG = DVO_HARRIS_GROUPS;
 __host__ __device__ inline int harris_blocks_x(const Plan& pl) {
     int hb = 0;
     for (int l = 0; l < pl.nlevels; ++l) hb = hb > 2 * pl.L[l].nper ? hb : 2 * pl.L[l].nper;
-    return (hb + 15) / 16 + 1;
+    return (hb + 16 * kHG - 1) / (16 * kHG) + 1;
 }
 
 __global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
-    __shared__ uint32_t win[16][32];  // one 9 x 3-word window (+ padding) per 16-lane group
+    __shared__ uint32_t win[kHG][16][32];  // one 9 x 3-word window (+ padding) per 16-lane group
     const int l = blockIdx.y, f = blockIdx.z;
     const int hb = blockIdx.x, gdx = gridDim.x;
     const int n = P.buf.cnt1[f * kMaxLevels + l];
@@ -1192,49 +1199,60 @@ __global__ __launch_bounds__(256) void harris_kernel(StreamParams P) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 4, j = lane & 15;
-    uint32_t* W = win[wid * 4 + g];
-    const uint8_t* Wb = reinterpret_cast<const uint8_t*>(W);
     const uint32_t* cand = P.buf.cand + (int64_t)f * P.plan.cand_stride + G.cand_off;
     float* resp = P.buf.resp + (int64_t)f * P.plan.cand_stride + G.cand_off;
-    for (int base = (hb * 4 + wid) * 4; base < n; base += gdx * 16) {
-        const int i = min(base + g, n - 1);
-        const uint32_t key = cand[i];
-        const int x0 = key & 0xFFF, y0 = (key >> 12) & 0xFFF;
-        const int ax = (x0 - 4) & ~3;  // window columns ax .. ax+11 cover x0-4 .. x0+4
-        const uint8_t* wp = img + (int64_t)(y0 - 4) * step + ax;
-        const int e1 = min(j + 16, 26);
-        const uint32_t v0 = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(j / 3) * step + 4 * (j % 3));
-        const uint32_t v1 = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(e1 / 3) * step + 4 * (e1 % 3));
-        __builtin_amdgcn_wave_barrier();
-        W[j] = v0;
-        W[j + 16] = v1;  // j + 16 >= 27: padding words
-        __builtin_amdgcn_wave_barrier();
-        const int o = x0 - ax - 3;  // window column of block column 0 (pixel x0 - 3)
-        int a = 0, b = 0, c = 0;
+    for (int base = (hb * 4 + wid) * 4 * kHG; base < n; base += gdx * 16 * kHG) {
+        int x0[kHG], ax[kHG];
+        uint32_t v0[kHG], v1[kHG];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int pos = j + 16 * t;
-            if (t < 3 || pos < 49) {
-                const int py = pos / 7, px = pos - 7 * py;
-                const uint8_t* q = Wb + (1 + py) * 12 + o + px;
-                const int Ix = (q[1] - q[-1]) * 2 + (q[-12 + 1] - q[-12 - 1]) + (q[12 + 1] - q[12 - 1]);
-                const int Iy = (q[12] - q[-12]) * 2 + (q[12 - 1] - q[-12 - 1]) + (q[12 + 1] - q[-12 + 1]);
-                a += Ix * Ix;
-                b += Iy * Iy;
-                c += Ix * Iy;
+        for (int u = 0; u < kHG; ++u) {  // group u: keypoints base + 4 u .. base + 4 u + 3
+            const int i = min(base + 4 * u + g, n - 1);
+            const uint32_t key = cand[i];
+            x0[u] = key & 0xFFF;
+            const int y0 = (key >> 12) & 0xFFF;
+            ax[u] = (x0[u] - 4) & ~3;  // window columns ax .. ax+11 cover x0-4 .. x0+4
+            const uint8_t* wp = img + (int64_t)(y0 - 4) * step + ax[u];
+            const int e1 = min(j + 16, 26);
+            v0[u] = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(j / 3) * step + 4 * (j % 3));
+            v1[u] = *reinterpret_cast<const uint32_t*>(wp + (int64_t)(e1 / 3) * step + 4 * (e1 % 3));
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < kHG; ++u) {
+            win[u][wid * 4 + g][j] = v0[u];
+            win[u][wid * 4 + g][j + 16] = v1[u];  // j + 16 >= 27: padding words
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < kHG; ++u) {
+            const uint8_t* Wb = reinterpret_cast<const uint8_t*>(win[u][wid * 4 + g]);
+            const int o = x0[u] - ax[u] - 3;  // window column of block column 0 (pixel x0 - 3)
+            int a = 0, b = 0, c = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int pos = j + 16 * t;
+                if (t < 3 || pos < 49) {
+                    const int py = pos / 7, px = pos - 7 * py;
+                    const uint8_t* q = Wb + (1 + py) * 12 + o + px;
+                    const int Ix = (q[1] - q[-1]) * 2 + (q[-12 + 1] - q[-12 - 1]) + (q[12 + 1] - q[12 - 1]);
+                    const int Iy = (q[12] - q[-12]) * 2 + (q[12 - 1] - q[-12 - 1]) + (q[12 + 1] - q[-12 + 1]);
+                    a += Ix * Ix;
+                    b += Iy * Iy;
+                    c += Ix * Iy;
+                }
             }
-        }
 #pragma unroll
-        for (int s2 = 8; s2 >= 1; s2 >>= 1) {
-            a += __shfl_xor(a, s2);
-            b += __shfl_xor(b, s2);
-            c += __shfl_xor(c, s2);
-        }
-        if (j == 0 && base + g < n) {
-            const float scale = 1.f / ((1 << 2) * 7 * 255.f);
-            const float s4 = scale * scale * scale * scale;
-            const float fa = (float)a, fb = (float)b, fc = (float)c;
-            resp[base + g] = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+            for (int s2 = 8; s2 >= 1; s2 >>= 1) {
+                a += __shfl_xor(a, s2);
+                b += __shfl_xor(b, s2);
+                c += __shfl_xor(c, s2);
+            }
+            if (j == 0 && base + 4 * u + g < n) {
+                const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+                const float s4 = scale * scale * scale * scale;
+                const float fa = (float)a, fb = (float)b, fc = (float)c;
+                resp[base + 4 * u + g] = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
