@@ -1326,7 +1326,7 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // samples are then LDS reads.
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
 #ifndef DVO_DKW
-#define DVO_DKW 1
+#define DVO_DKW 2  // keypoints per wave, loads of all requested first: 1 73.0 K, 2 73.6 K, 4 72.3 K frames/s (profiles/r02z_ab_describe_dkw.txt)
 #endif
 constexpr int kDKW = DVO_DKW;          // keypoints per wave
 constexpr int kDKB = 4 * kDKW;         // keypoints per workgroup
@@ -1392,11 +1392,42 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         keys[kk] = P.buf.cand[(int64_t)f * P.plan.cand_stride + P.plan.L[l].cand_off + i];
         resps[kk] = P.buf.resp[(int64_t)f * P.plan.cand_stride + P.plan.L[l].cand_off + i];
     }
-    // ---- phase 1: per keypoint of this wave, fetch both windows, IC angle
+    // ---- phase 1: every keypoint of this wave requests both windows first (one load latency
+    // covers the wave's kDKW keypoints), then each is staged in LDS and gets its IC angle
+    constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
+    uint32_t ivs[kDKW][5], pvs[kDKW][7];
+#pragma unroll
+    for (int kk = 0; kk < kDKW; ++kk) {  // slots past nk read the clamped last keypoint (unused)
+        const int l = lv[kk];
+        const LevelGeom& G = P.plan.L[l];
+        const uint32_t key = keys[kk];
+        const int kx = key & 0xFFF, ky = (key >> 12) & 0xFFF;
+        const float scale = G.scale;
+        const float sc = 1.f / scale;
+        const int cxb = cv_round_f((float)kx * scale * sc), cyb = cv_round_f((float)ky * scale * sc);
+        const int a0 = (cxb - kDPR) & ~3;
+        const int ai = (kx - 15) & ~3;
+        const int step = level_pitch(P, l);
+        const uint8_t* img = level_ptr(P, f, l) + (int64_t)(ky - 15) * step + ai;
+        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const int ec = min(64 * t + lane, kIW - 1);
+            const int rc = ec / (kICW / 4), wc = ec - rc * (kICW / 4);
+            ivs[kk][t] = *reinterpret_cast<const uint32_t*>(img + (int64_t)rc * step + 4 * wc);
+        }
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int ec = min(64 * t + lane, kPW - 1);
+            const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
+            pvs[kk][t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
+        }
+    }
+#pragma unroll
     for (int kk = 0; kk < kDKW; ++kk) {
         const int slot = wv * kDKW + kk;
         const int k = bxi * kDKB + slot;
-        if (k >= nk) break;  // wave-uniform
+        if (k >= nk) continue;  // wave-uniform
         const int l = lv[kk];
         const LevelGeom& G = P.plan.L[l];
         const uint32_t key = keys[kk];
@@ -1404,34 +1435,15 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         const float scale = G.scale;
         const float ptx = (float)kx * scale, pty = (float)ky * scale;
         const float sc = 1.f / scale;
-        const int cxb = cv_round_f(ptx * sc), cyb = cv_round_f(pty * sc);  // orb.cpp: center = &img(cvRound(pt*sc))
+        const int cxb = cv_round_f(ptx * sc);  // orb.cpp: center = &img(cvRound(pt*sc))
         const int a0 = (cxb - kDPR) & ~3;
         const int ai = (kx - 15) & ~3;
-        {  // all 5 IC-window and 7 patch word loads in flight (clamped loads, padded stores)
-            const uint8_t* img = level_ptr(P, f, l) + (int64_t)(ky - 15) * level_pitch(P, l) + ai;
-            const int step = level_pitch(P, l);
-            const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
-            constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
-            uint32_t iv[5], pv[7];
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int t = 0; t < 5; ++t) {
-                const int ec = min(64 * t + lane, kIW - 1);
-                const int rc = ec / (kICW / 4), wc = ec - rc * (kICW / 4);
-                iv[t] = *reinterpret_cast<const uint32_t*>(img + (int64_t)rc * step + 4 * wc);
-            }
+        for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
 #pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                const int ec = min(64 * t + lane, kPW - 1);
-                const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
-                pv[t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
-            }
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = iv[t];
-#pragma unroll
-            for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pv[t];
-            __builtin_amdgcn_wave_barrier();
-        }
+        for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pvs[kk][t];
+        __builtin_amdgcn_wave_barrier();
         // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
         const uint8_t* col = &icw[wv][0][0] + (kx - ai) + u;
         int sI = 0, m01 = 0;
