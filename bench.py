@@ -8,9 +8,10 @@ is the previous batch's last frame), Hamming cross-check matching,
 findEssentialMat (RANSAC, 5-point), recoverPose and the marker-scaled pose tail
 (triangulated marker corners -> scale -> 4x4 relative pose -> chained absolute
 pose) for the B consecutive pairs.  With N > 1 ranks (configs[3]) ONE stream is
-sharded: each rank takes B consecutive pairs of a window of N x B plus a halo
-pair, the ranks all-gather records and relative poses over RCCL, and rank 0
-chains the window's absolute poses (main_sharded).
+sharded: each rank takes B consecutive pairs of a window of N x B, the ranks
+all-gather their pair records and marker corners over RCCL, and rank 0 runs the
+window's marker-scaled pose tail and absolute chain (SURVEY.md §8e;
+main_sharded).
 value = (B x steps x ranks) / max-over-ranks wall time.
 
 Also reported:
@@ -59,6 +60,9 @@ def parse():
     ap.add_argument("--host-trace", action="store_true", help="print host-side enqueue times per step to stderr")
     ap.add_argument("--dropin-seconds", type=float, default=4.0,
                     help="bounded timing of the per-pair drop-in surface (0 = skip)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="take the sharded path (main_sharded) even at N=1: rehearses the RCCL exchange and its "
+                         "stream ordering on one GPU")
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight: each on its own dvo_stream / HIP stream, so one batch's "
                          "serial RANSAC tail overlaps the next batch's ORB")
@@ -97,8 +101,9 @@ def main():
     backend = os.environ.get("DVO_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local_rank = local_rank % torch.cuda.device_count()
-    if world > 1:
+    if world > 1 or args.sharded:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         torch.cuda.set_device(local_rank)
         if backend == "gloo":
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -113,7 +118,7 @@ def main():
 
     W, H, N, B = args.width, args.height, args.nfeatures, args.batch
     scene = SceneStream(W, H, device=str(dev))
-    if world > 1:
+    if world > 1 or args.sharded:
         return main_sharded(args, world, rank, local_rank, backend, dev, scene)
     pool_n = args.pool or (2 * B + 1)
     pool = torch.stack([scene.render(i) for i in range(pool_n)]).contiguous()
@@ -274,62 +279,42 @@ def main():
 def main_sharded(args, world, rank, local_rank, backend, dev, scene):
     """N > 1 (BASELINE configs[3]): ONE stream sharded across the ranks.  A step
     is a window of world x B consecutive pairs; rank r computes pairs
-    [r B, (r+1) B) of it plus the halo pair before them (dist.shard_window),
-    the ranks all-gather their 256-B records and T_rel rows over RCCL
-    (dist.ShardedPoseStream), and rank 0 chains the window's absolute poses on
-    the device (stream.PoseChain), continuing the chain across steps.  Weak
-    scaling: B new pairs per rank per step; value = world x B x steps / time."""
+    [r B, (r+1) B) of it (frames r B .. (r+1) B, dist.shard_window) into the
+    record slots of its send buffer, the ranks all-gather records and marker
+    corners in one collective over RCCL (dist.ShardedPoseStream), and rank 0
+    runs the window's pose tail -- marker scale against the previous
+    successful pair, relative pose, absolute chain -- from the gathered
+    records (stream.PoseTail), continuing across steps.  Weak scaling: B new
+    pairs per rank per step; value = world x B x steps / max-over-ranks time.
+
+    Stream ordering on the RCCL path (no host syncs in the loop): torch's
+    stream waits for the library stream's records before the collective, and
+    the library stream waits for the collective's `done` event before it
+    rewrites the same send buffer S steps later."""
     import torch
     import torch.distributed as dist
     from droplet_visual_odometry_amd import dist as ddist
     from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE, Context
-    from droplet_visual_odometry_amd.stream import FrameStream, PoseChain
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     W, H, N, B = args.width, args.height, args.nfeatures, args.batch
     WP = world * B
     n_windows = 2
     wins = [ddist.shard_window(WP, world, rank, j * WP) for j in range(n_windows)]
     # each rank renders only the frames of its own runs (no scatter)
-    pools = [torch.stack([scene.render(g) for g in range(f0, f1)]).contiguous() for (_, _, f0, f1, _) in wins]
+    pools = [torch.stack([scene.render(g) for g in range(f0, f1)]).contiguous() for (_, _, f0, f1) in wins]
     corners = [torch.tensor(np.stack([scene.marker_corners(g) for g in range(f0, f1)]), dtype=torch.float64,
-                            device=dev) for (_, _, f0, f1, _) in wins]
+                            device=dev) for (_, _, f0, f1) in wins]
     torch.cuda.synchronize()
-    ctx = Context(local_rank)
-    S = max(1, args.streams)
-    host_gather = backend == "gloo"
-    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 2, max_iters=args.max_iters, ctx=ctx)
-           for _ in range(S)]
-    shs = [ddist.ShardedPoseStream(world, rank, WP, dev, host_gather=host_gather) for _ in range(S)]
-    recs_t = [f.new_records(B + 1) for f in fss]
-    T_rel = [torch.zeros((B + 1, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-    T_loc = [torch.zeros((B + 1, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-    for f in fss:
-        f.reset_pose()
-    chain = PoseChain(ctx) if rank == 0 else None
-    T_abs = [torch.empty((WP, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)] if rank == 0 else None
+    run = ddist.ShardedStreamRunner(W, H, scene.K, N, WP, world, rank, MARKER_LEN, ctx=Context(local_rank),
+                                    max_iters=args.max_iters, streams=args.streams, host_gather=backend == "gloo")
+    S = run.S
     torch.cuda.synchronize()
 
     def step(i):
-        j, k = i % n_windows, i % S
-        fs = fss[k]
-        fr, c = pools[j], corners[j]
-        halo = wins[j][4]
-        fs.process(fr, recs_t[k], wait_torch=False)
-        fs.pose_tail(c[:-1], c[1:], MARKER_LEN, T_rel[k], T_loc[k], wait_torch=False)
-        if host_gather:
-            fs.sync()
-        else:
-            # RCCL (on torch's stream) reads the records once the library's stream has written them
-            torch.cuda.current_stream().wait_event(fs.record_event())
-        _, all_T = shs[k].exchange(recs_t[k], T_rel[k], halo)
-        if rank == 0:
-            chain.run(all_T.to(dev, non_blocking=True) if host_gather else all_T, T_abs[k])
+        j = i % n_windows
+        return run.step(pools[j], corners[j][:-1], corners[j][1:])[0]
 
-    def sync_all():
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
-
+    sync_all = run.sync
     for i in range(args.warmup):
         step(i)
     sync_all()
@@ -337,16 +322,14 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        recs = step(args.warmup + i)
     sync_all()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if host_gather else dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if run.host_gather else dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    last = (args.warmup + args.steps - 1) % S
-    all_rec, _ = shs[last].exchange(recs_t[last], T_rel[last], wins[(args.warmup + args.steps - 1) % n_windows][4])
-    recs = all_rec.cpu().numpy().view(PAIR_RECORD_DTYPE)
+    recs = recs.cpu().numpy().view(PAIR_RECORD_DTYPE)
     value = WP * args.steps / elapsed
     if rank == 0:
         m_avg = float(np.mean(recs["n_matches"]))
@@ -366,11 +349,11 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
             "dtype": "u8/f32/f64",
             "data": "synthetic (seeded ray-cast textured room, droplet_visual_odometry_amd/synth.py)",
             "config": {"workload": f"{W}x{H} mono8 stream, {N} ORB features, one stream sharded over {world} "
-                                   f"ranks, {B} new frames/step per rank (+1 halo pair)",
+                                   f"ranks, {B} new frames/step per rank",
                        "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
                        "parallelism": f"one stream pair-sharded x{world} + "
-                                      + ("gloo all_gather (rehearsal)" if host_gather else "RCCL all_gather")
-                                      + " of records and T_rel, rank-0 device pose chain",
+                                      + ("gloo all_gather (rehearsal)" if run.host_gather else "RCCL all_gather")
+                                      + " of records and marker corners, rank-0 device pose tail and chain",
                        "streams_in_flight": S,
                        "pairs_ok": f"{int(np.sum(recs['status'] == 0))}/{len(recs)}", "mean_matches": round(m_avg, 1),
                        "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1)},

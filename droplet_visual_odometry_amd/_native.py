@@ -54,7 +54,8 @@ class DVOError(RuntimeError):
 class OrbParams(ctypes.Structure):
     _fields_ = [("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int32),
                 ("edge_threshold", ctypes.c_int32), ("first_level", ctypes.c_int32), ("wta_k", ctypes.c_int32),
-                ("score_type", ctypes.c_int32), ("patch_size", ctypes.c_int32), ("fast_threshold", ctypes.c_int32)]
+                ("score_type", ctypes.c_int32), ("patch_size", ctypes.c_int32), ("fast_threshold", ctypes.c_int32),
+                ("opencv_semantics", ctypes.c_int32)]
 
 
 class StreamConfig(ctypes.Structure):
@@ -64,10 +65,25 @@ class StreamConfig(ctypes.Structure):
                 ("dist_thresh", ctypes.c_double)]
 
 
+# OpenCV semantics of the ORB path (include/dvo.h DVO_OPENCV_*): "4.x" (default) or "3.2"
+OPENCV_SEMANTICS = {"4.x": 0, "3.2": 1}
+
+
+def opencv_semantics(v) -> int:
+    if isinstance(v, str):
+        if v not in OPENCV_SEMANTICS:
+            raise ValueError(f"opencv semantics must be one of {sorted(OPENCV_SEMANTICS)}")
+        return OPENCV_SEMANTICS[v]
+    if int(v) not in OPENCV_SEMANTICS.values():
+        raise ValueError(f"opencv semantics must be one of {sorted(OPENCV_SEMANTICS)}")
+    return int(v)
+
+
 def orb_params(nfeatures=500, scale_factor=1.2, nlevels=8, edge_threshold=31, first_level=0, wta_k=2,
-               score_type=0, patch_size=31, fast_threshold=20) -> OrbParams:
+               score_type=0, patch_size=31, fast_threshold=20, opencv="4.x") -> OrbParams:
     return OrbParams(int(nfeatures), float(np.float32(scale_factor)), int(nlevels), int(edge_threshold),
-                     int(first_level), int(wta_k), int(score_type), int(patch_size), int(fast_threshold))
+                     int(first_level), int(wta_k), int(score_type), int(patch_size), int(fast_threshold),
+                     opencv_semantics(opencv))
 
 
 _vp = ctypes.c_void_p
@@ -106,12 +122,13 @@ _SIGNATURES = {
     "dvo_stream_process_undistorted": ([_vp, _vp, _vp, _c, _i64, _c, _vp], _c),
     "dvo_stream_share_pose": ([_vp, _vp], _c),
     "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
+    "dvo_pose_tail_records": ([_vp, _vp, _c, _vp, _vp, _vp, _c, _d, _vp, _vp, _vp, _vp], _c),
     "dvo_pose_chain": ([_vp, _vp, _c, _vp, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),
     "dvo_stream_get_features": ([_vp, _c, _vp, _vp, _c, _ip], _c),
     "dvo_stream_get_matches": ([_vp, _c, _vp, _c, _ip], _c),
     "dvo_stream_get_pyramid": ([_vp, _c, _c, _c, _vp, _c], _c),
-    "dvo_test_retain_best": ([_vp, _vp, _c, _c, _c, _vp, _ip], _c),
+    "dvo_test_retain_best": ([_vp, _vp, _c, _c, _c, _c, _vp, _ip], _c),
     "dvo_test_update_num_iters": ([_vp, _d, _vp, _c, _c, _c, _vp], _c),
     "dvo_test_five_point": ([_vp, _vp, _vp, _vp, _ip], _c),
     "dvo_test_ransac_subsets": ([_vp, _c, _c, _vp], _c),

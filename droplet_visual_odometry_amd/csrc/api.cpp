@@ -65,6 +65,7 @@ struct dvo_stream {
     bool own_hs = false;
     int last_nframes = 0;
     bool last_has_pairs = false;  // the last call ran match + geometry
+    const dvo_pair_record* last_rec = nullptr;  // the caller's records of that call (read by the pose tail)
     hipStream_t hs = nullptr;
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
@@ -106,8 +107,21 @@ void features_per_level(int nfeatures, int nlevels, int* out) {
     out[nlevels - 1] = std::max(nfeatures - sum, 0);
 }
 
-Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
+// OpenCV 3.2 resize(INTER_LINEAR) on x86: VResizeLinearVec_32s8u (SSE2) covers
+// the columns before the point where its 16-wide loop (x <= W - 16) and then
+// its 4-wide loop (x < W - 4) stop; VResizeLinear's scalar loop does the rest.
+int ocv32_simd_end(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {
+    }
+    for (; x < width - 4; x += 4) {
+    }
+    return x;
+}
+
+Plan make_plan(int w, int h, int nfeatures, int fast_threshold, int semantics) {
     Plan p{};
+    p.semantics = semantics;
     p.w = w;
     p.h = h;
     p.nlevels = kMaxLevels;
@@ -116,7 +130,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     int nper[kMaxLevels];
     features_per_level(nfeatures, kMaxLevels, nper);
     int64_t pyr = 0, blur = 0, bcand = 0, cand = 0;
-    int bands = 0, strips = 0, tiles = 0, coef = 0;
+    int bands = 0, strips = 0, tiles = 0, coef = 0, coef32 = 0;
     for (int l = 0; l < kMaxLevels; ++l) {
         LevelGeom& G = p.L[l];
         G.scale = (float)std::pow((double)1.2f, (double)l);  // getScale
@@ -134,6 +148,10 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
         G.xcoef_off = l == 0 ? 0 : coef;
         G.ycoef_off = l == 0 ? 0 : coef + ((G.w + 3) & ~3);
         if (l > 0) coef += ((G.w + 3) & ~3) + ((G.h + 7) & ~7);  // y table padded to 8 rows (resize_level_lds_kernel)
+        G.l32_x = l == 0 ? 0 : coef32;
+        G.l32_y = l == 0 ? 0 : coef32 + 4 * G.w;
+        if (l > 0) coef32 += 4 * (G.w + G.h);
+        G.l32_xs = ocv32_simd_end(G.w);
         const bool usable = G.w > 2 * kBorder && G.h > 2 * kBorder;
         const int rows = usable ? G.h - 2 * kBorder : 0;
         const int wc = usable ? G.w - 2 * kBorder : 0;
@@ -162,6 +180,7 @@ Plan make_plan(int w, int h, int nfeatures, int fast_threshold) {
     p.cand_stride = (cand + 63) & ~(int64_t)63;
     p.total_tiles = tiles;
     p.coef_total = coef;
+    p.coef32_total = coef32;
     p.kp_cap = ((nfeatures + 256) + 63) & ~63;
     return p;
 }
@@ -196,6 +215,54 @@ std::vector<int32_t> resize_coefs(const Plan& p) {
     return c;
 }
 
+// OpenCV 3.2 resize(INTER_LINEAR) tables (imgwarp.cpp resize; oracle/orb.cpp
+// resize_linear_32): fx = (float)((d + 0.5) * scale - 0.5) in double rounded to
+// float, sx = cvFloor(fx), weights saturate_cast<short>(w * 2048.f) each
+// rounded half to even.  Columns: {sx, sx + 1, a0 | a1 << 16, 0}, the
+// positions past xmax {W-1, W-1, 2048, 0}; rows: {clip(sy), clip(sy + 1),
+// b0 | b1 << 16, 0}.
+std::vector<int32_t> resize_coefs_32(const Plan& p) {
+    std::vector<int32_t> c(std::max(p.coef32_total, 4));
+    auto wgt = [](float v) { return (int32_t)std::max(-32768, std::min(32767, cv_round_f(v))); };
+    for (int l = 1; l < p.nlevels; ++l) {
+        const LevelGeom &S = p.L[l - 1], &D = p.L[l];
+        const double sx_scale = 1. / ((double)D.w / S.w), sy_scale = 1. / ((double)D.h / S.h);
+        int xmax = D.w;
+        for (int dx = 0; dx < D.w; ++dx) {
+            float fx = (float)((dx + 0.5) * sx_scale - 0.5);
+            int sx = (int)std::floor(fx);
+            fx -= (float)sx;
+            if (sx < 0) fx = 0, sx = 0;
+            if (sx + 1 >= S.w) {
+                xmax = std::min(xmax, dx);
+                if (sx >= S.w - 1) fx = 0, sx = S.w - 1;
+            }
+            int32_t* e = &c[D.l32_x + 4 * dx];
+            if (dx < xmax) {
+                e[0] = sx;
+                e[1] = sx + 1;
+                e[2] = (wgt((1.f - fx) * 2048) & 0xFFFF) | (wgt(fx * 2048) << 16);
+            } else {
+                e[0] = e[1] = sx;
+                e[2] = 2048;
+            }
+            e[3] = 0;
+        }
+        auto clip = [](int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; };
+        for (int dy = 0; dy < D.h; ++dy) {
+            float fy = (float)((dy + 0.5) * sy_scale - 0.5);
+            const int sy = (int)std::floor(fy);
+            fy -= (float)sy;
+            int32_t* e = &c[D.l32_y + 4 * dy];
+            e[0] = clip(sy, 0, S.h);
+            e[1] = clip(sy + 1, 0, S.h);
+            e[2] = (wgt((1.f - fy) * 2048) & 0xFFFF) | (wgt(fy * 2048) << 16);
+            e[3] = 0;
+        }
+    }
+    return c;
+}
+
 int check_orb_params(dvo_ctx* ctx, const dvo_orb_params* o) {
     if (!o) return fail(ctx, DVO_EINVAL, "null ORB parameters");
     if (o->nfeatures <= 0 || o->nfeatures > 7680) return fail(ctx, DVO_EINVAL, "nfeatures out of range (1..7680)");
@@ -205,6 +272,8 @@ int check_orb_params(dvo_ctx* ctx, const dvo_orb_params* o) {
                     "only cv.ORB_create() defaults (scaleFactor 1.2, nlevels 8, edgeThreshold 31, firstLevel 0, "
                     "WTA_K 2, HARRIS_SCORE, patchSize 31) are implemented");
     if (o->fast_threshold < 0 || o->fast_threshold > 255) return fail(ctx, DVO_EINVAL, "fastThreshold out of range");
+    if (o->opencv_semantics != DVO_OPENCV_4X && o->opencv_semantics != DVO_OPENCV_32)
+        return fail(ctx, DVO_EINVAL, "opencv_semantics must be DVO_OPENCV_4X or DVO_OPENCV_32");
     return DVO_OK;
 }
 
@@ -344,6 +413,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.pyr, (size_t)F * p.pyr_stride);
     A(b.blur, (size_t)F * p.blur_stride);
     A(b.coef, (size_t)std::max(p.coef_total, 1));
+    A(b.coef32, (size_t)std::max(p.coef32_total, 4));
     A(b.band_cnt, (size_t)F * (p.total_bands + 1) * kBandRows);
     A(b.band_cand, (size_t)F * p.band_cand_stride);
     A(b.cand, (size_t)F * p.cand_stride);
@@ -444,6 +514,7 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     HIP_TRY(launch_orb(P, s->hs, ev));
     s->last_nframes = n;
     s->last_has_pairs = !detect_only && n >= 2;
+    s->last_rec = d_rec;
     if (!s->last_has_pairs) return DVO_OK;
     HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, ev));
     GeomArgs g = stream_geom(s);
@@ -511,7 +582,7 @@ int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** o
     auto s = std::make_unique<dvo_stream>();
     s->ctx = ctx;
     s->cfg = *cfg;
-    s->plan = make_plan(cfg->width, cfg->height, cfg->orb.nfeatures, cfg->orb.fast_threshold);
+    s->plan = make_plan(cfg->width, cfg->height, cfg->orb.nfeatures, cfg->orb.fast_threshold, cfg->orb.opencv_semantics);
     if (s->plan.kp_cap > 65535) return fail(ctx, DVO_EINVAL, "too many features");
     if (hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking) != hipSuccess)
         return fail(ctx, DVO_EHIP, "hipStreamCreate failed");
@@ -523,8 +594,10 @@ int dvo_stream_create(dvo_ctx* ctx, const dvo_stream_config* cfg, dvo_stream** o
     }
     rc = stream_alloc(s.get());
     if (!rc) {
-        const std::vector<int32_t> coefs = resize_coefs(s->plan);
-        if (hipMemcpy(s->buf.coef, coefs.data(), coefs.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess)
+        const std::vector<int32_t> coefs = resize_coefs(s->plan), coefs32 = resize_coefs_32(s->plan);
+        if (hipMemcpy(s->buf.coef, coefs.data(), coefs.size() * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(s->buf.coef32, coefs32.data(), coefs32.size() * sizeof(int32_t), hipMemcpyHostToDevice) !=
+                hipSuccess)
             rc = fail(ctx, DVO_EHIP, "coefficient upload failed");
     }
     if (rc) {
@@ -584,11 +657,25 @@ int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const doub
     dvo_stream* o = s->carry_owner;  // pose tails on one carry run in call order, across streams
     if (o->carry_ev_valid) HIP_TRY(hipStreamWaitEvent(s->hs, o->carry_ev, 0));
     mark(ev, 8, 0, s->hs);
-    HIP_TRY(launch_pose_tail(s->buf.Rt, s->buf.info, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
+    HIP_TRY(launch_pose_tail(s->last_rec, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
                              o->d_carry, d_T_rel, d_T_abs, s->hs));
     mark(ev, 8, 1, s->hs);
     HIP_TRY(hipEventRecord(o->carry_ev, s->hs));
     o->carry_ev_valid = true;
+    return DVO_OK;
+}
+
+int dvo_pose_tail_records(dvo_ctx* ctx, const dvo_pair_record* d_records, int pairs, const double* K,
+                          const double* d_corners_prev, const double* d_corners_cur, int k, double marker_length,
+                          double* d_carry, double* d_T_rel, double* d_T_abs, void* hip_stream) {
+    if (!ctx) return DVO_EINVAL;
+    if (pairs < 0 || !K) return fail(ctx, DVO_EINVAL, "pose tail needs pairs >= 0 and K");
+    if (pairs == 0) return DVO_OK;
+    if (k < 2 || !d_records || !d_corners_prev || !d_corners_cur || !d_carry || !d_T_rel || !d_T_abs)
+        return fail(ctx, DVO_EINVAL, "pose tail needs records, >= 2 corners per frame, the carry and output buffers");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(launch_pose_tail(d_records, pairs, K, d_corners_prev, d_corners_cur, k, marker_length, d_carry, d_T_rel,
+                             d_T_abs, hip_stream ? (hipStream_t)hip_stream : ctx->stream));
     return DVO_OK;
 }
 
@@ -722,7 +809,8 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
     if (w < 8 || h < 8 || w >= kMaxW || h >= kMaxW) return fail(ctx, DVO_EINVAL, "image size out of range (8..4095)");
     HIP_TRY(hipSetDevice(ctx->device));
     if (!ctx->call_stream || ctx->call_w != w || ctx->call_h != h || ctx->call_nf != params->nfeatures ||
-        ctx->call_stream->cfg.orb.fast_threshold != params->fast_threshold) {
+        ctx->call_stream->cfg.orb.fast_threshold != params->fast_threshold ||
+        ctx->call_stream->cfg.orb.opencv_semantics != params->opencv_semantics) {
         if (ctx->call_stream) dvo_stream_destroy(ctx->call_stream);
         ctx->call_stream = nullptr;
         dvo_stream_config cfg{};
@@ -1285,8 +1373,10 @@ int dvo_triangulate_points(dvo_ctx* ctx, const double* P1, const double* P2, con
 }
 
 // ---------------------------------------------------------------------------
-int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int32_t* perm, int* k_out) {
+int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int semantics,
+                         int32_t* perm, int* k_out) {
     if (!ctx || !resp || !perm || !k_out || n < 0) return DVO_EINVAL;
+    if (semantics != DVO_OPENCV_4X && semantics != DVO_OPENCV_32) return fail(ctx, DVO_EINVAL, "bad semantics");
     HIP_TRY(hipSetDevice(ctx->device));
     void *dv, *dk, *dt, *dkk;
     int rc;
@@ -1299,7 +1389,8 @@ int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, i
         HIP_TRY(hipMemcpy(dv, resp, (size_t)n * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(dk, ids.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     }
-    HIP_TRY(launch_test_retain_best((float*)dv, (uint32_t*)dk, (int32_t*)dt, n, n_points, depth, (int*)dkk, ctx->stream));
+    HIP_TRY(launch_test_retain_best((float*)dv, (uint32_t*)dk, (int32_t*)dt, n, n_points, depth, semantics, (int*)dkk,
+                                    ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     int k = 0;
     HIP_TRY(hipMemcpy(&k, dkk, sizeof(int), hipMemcpyDeviceToHost));

@@ -16,6 +16,8 @@ namespace dvo {
 
 
 constexpr int kMaxLevels = 8;
+// OpenCV semantics of the ORB path (dvo_orb_params.opencv_semantics): 4.x or 3.2.
+constexpr int kOcv4 = DVO_OPENCV_4X, kOcv32 = DVO_OPENCV_32;
 // FAST tile height (output rows).  Two-stream bench, 1280x720: 16 rows 66.8-67.2 K
 // frames/s, 20: 67.7 K, 24: 68.2-69.1 K, 28: 65.7-66.1 K, 32: 67.1-67.9 K
 // (taller tiles: fewer barriers and carried rows per output row, more LDS per
@@ -52,6 +54,8 @@ struct LevelGeom {
     int64_t cand_off;     // u32 offset of this level's gathered list within a frame
     int tile_base;        // first blur tile of this level within a frame
     int tiles_x, tiles_y; // blur tiling
+    int l32_x, l32_y;     // OpenCV 3.2 INTER_LINEAR tables of level l (l >= 1) in Buffers::coef32 (int4 entries)
+    int l32_xs;           // columns below this take 3.2's SSE2 vertical pass, the rest the scalar one
 };
 
 struct Plan {
@@ -65,6 +69,8 @@ struct Plan {
     int64_t cand_stride;      // u32 per frame
     int total_tiles;          // blur tiles per frame
     int coef_total;           // ints in the resize coefficient table
+    int coef32_total;         // ints in the OpenCV 3.2 resize tables
+    int semantics;            // kOcv4 / kOcv32
 };
 
 // Resize coefficient of one destination column/row (resize.cpp INTER_LINEAR_EXACT):
@@ -100,6 +106,7 @@ struct Buffers {
     uint8_t* pyr;
     uint8_t* blur;
     int32_t* coef;        // resize coefficient tables (Plan::coef_total ints)
+    int32_t* coef32;      // OpenCV 3.2 resize tables (Plan::coef32_total ints)
     int32_t* band_cnt;    // [F][total_bands][kBandRows] FAST keeps per tile row
     uint32_t* band_cand;
     uint32_t* cand;       // gathered candidate keys (score<<24 | y<<12 | x)
@@ -290,8 +297,8 @@ hipError_t launch_undistort_remap(const UndistortGeom& U, const int16_t* d_xy, c
                                   int64_t dst_fstride, int dst_pitch, hipStream_t s);
 
 // carry: device [12 P_prev | 16 T_abs_prev]; updated in place.
-hipError_t launch_pose_tail(const double* Rt /*[pairs][12]*/, const int32_t* info /*[pairs][4]*/, int pairs,
-                            const double* K, const double* cprev, const double* ccur, int k, double marker_length,
+// rec: the pairs' records (R, t, status, n_models are read).
+hipError_t launch_pose_tail(const dvo_pair_record* rec, int pairs, const double* K, const double* cprev, const double* ccur, int k, double marker_length,
                             double* carry, double* T_rel, double* T_abs, hipStream_t s);
 // T_abs[p] = T_carry . T_rel[0] ... T_rel[p] in pair order (the pose_tail chain on
 // its own: the reassembled pose stream of a sharded run); T_carry is updated.
@@ -317,7 +324,7 @@ hipError_t launch_surf(const SurfArgs& a, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
-                                   int* d_k, hipStream_t s);
+                                   int semantics, int* d_k, hipStream_t s);
 hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int model_points, int max_iters,
                                         int32_t* d_out, hipStream_t s);
 hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s);

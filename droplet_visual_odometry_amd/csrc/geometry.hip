@@ -2063,8 +2063,7 @@ __device__ void proj_of(const double* K, const double* Rt, double* P) {  // K . 
 }
 
 struct TailArgs {
-    const double* Rt;
-    const int32_t* info;
+    const dvo_pair_record* rec;  // R (9) and t (3) are the record's first 12 doubles: the [R | t] layout
     int pairs;
     double K[9];
     const double* cprev;
@@ -2077,31 +2076,37 @@ struct TailArgs {
     double* T_abs;
 };
 
+// A pair the reference gets through to the pose tail: findEssentialMat returned
+// exactly one E and recoverPose ran (status DVO_OK, one model).  Every other
+// record is a pair where the reference raises before v3:344.
+__device__ inline bool rec_ok(const dvo_pair_record* rec, int p) {
+    return rec[p].status == DVO_OK && rec[p].n_models == 1;
+}
+__device__ inline const double* rec_Rt(const dvo_pair_record* rec, int p) { return rec[p].R; }
+
+// The pose tail reads only the 256-B pair records (R, t, status), so a pose
+// stream whose records were computed on several ranks and all-gathered gives
+// the same result as one rank's (dvo_pose_tail_records).
 __global__ void pose_tail_kernel(TailArgs a) {
     const int p = blockIdx.x * 64 + threadIdx.x;
     if (p >= a.pairs) return;
     double* Tr = a.T_rel + (int64_t)p * 16;
-    const int32_t* inf = a.info + (int64_t)p * 4;
-    if (!(inf[3] == DVO_OK && inf[0] == 3)) {  // the reference would have raised here
+    if (!rec_ok(a.rec, p)) {  // the reference would have raised here
         for (int r = 0; r < 16; ++r) Tr[r] = (r % 5 == 0) ? 1.0 : 0.0;
         return;
     }
-    const double* Rt = a.Rt + (int64_t)p * 12;
+    const double* Rt = rec_Rt(a.rec, p);
     double Pc[12], Pp[12];
     proj_of(a.K, Rt, Pc);
     // P_prev is the projection of the last pair that got through (the reference
     // sets previous_projection_matrix only at the end of a successful pair,
     // v3:344); the carry when no earlier pair of this batch did.
     int q = p - 1;
-    while (q >= 0) {
-        const int32_t* iq = a.info + (int64_t)q * 4;
-        if (iq[3] == DVO_OK && iq[0] == 3) break;
-        --q;
-    }
+    while (q >= 0 && !rec_ok(a.rec, q)) --q;
     if (q < 0) {
         for (int r = 0; r < 12; ++r) Pp[r] = a.carry[r];
     } else {
-        proj_of(a.K, a.Rt + (int64_t)q * 12, Pp);
+        proj_of(a.K, rec_Rt(a.rec, q), Pp);
     }
     double X0[4], X1[4];
     const double* cp = a.cprev + (int64_t)p * a.k * 2;
@@ -2139,11 +2144,9 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
     __shared__ double tr[kChunk * 16];
     const int lane = threadIdx.x;
     int last_ok = -1;
-    if (a.info) {
-        for (int p = lane; p < a.pairs; p += 64) {
-            const int32_t* inf = a.info + (int64_t)p * 4;
-            if (inf[3] == DVO_OK && inf[0] == 3) last_ok = p;
-        }
+    if (a.rec) {
+        for (int p = lane; p < a.pairs; p += 64)
+            if (rec_ok(a.rec, p)) last_ok = p;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
     }
@@ -2189,7 +2192,7 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
         a.tcarry[r * 4 + 2] = t2;
         a.tcarry[r * 4 + 3] = t3;
     }
-    if (lane == 0 && last_ok >= 0 && a.carry) proj_of(a.K, a.Rt + (int64_t)last_ok * 12, a.carry);
+    if (lane == 0 && last_ok >= 0 && a.carry) proj_of(a.K, rec_Rt(a.rec, last_ok), a.carry);
 }
 
 __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, int mp, int mi, int32_t* out) {
@@ -2246,13 +2249,12 @@ hipError_t launch_triangulate(const double* d_P, const double* d_x, int k, doubl
     return hipGetLastError();
 }
 
-hipError_t launch_pose_tail(const double* Rt, const int32_t* info, int pairs, const double* K, const double* cprev,
+hipError_t launch_pose_tail(const dvo_pair_record* rec, int pairs, const double* K, const double* cprev,
                             const double* ccur, int k, double marker_length, double* carry, double* T_rel,
                             double* T_abs, hipStream_t s) {
     if (pairs <= 0) return hipSuccess;
     TailArgs a{};
-    a.Rt = Rt;
-    a.info = info;
+    a.rec = rec;
     a.pairs = pairs;
     for (int i = 0; i < 9; ++i) a.K[i] = K[i];
     a.cprev = cprev;

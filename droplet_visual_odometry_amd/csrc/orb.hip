@@ -268,8 +268,48 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
 }
 
 // ------------------------------------------------------------------------
+// OpenCV 3.2 semantics (Plan::semantics == kOcv32): ORB's pyramid was
+// resize(INTER_LINEAR), 11-bit weights, not INTER_LINEAR_EXACT (oracle/orb.cpp
+// resize_linear_32 restates it).  Per-plan tables (api.cpp resize_coefs_32):
+// per destination column {sx, sx1, a0 | a1 << 16} (past xmax: sx1 = sx, a0 =
+// 2048, a1 = 0, the HResizeLinear tail S[sx] * 2048) and per row {r0, r1,
+// b0 | b1 << 16} with the rows already clipped.  One thread per output pixel
+// (a parity mode, not the bench path): the two source rows are L2-resident.
+// The vertical pass takes the SSE2 form below column l32_xs, the scalar
+// FixedPtCast form from there on.
+__global__ __launch_bounds__(256) void resize_level_ocv32_kernel(StreamParams P, int l) {
+    const int f = blockIdx.z;
+    const LevelGeom& S = P.plan.L[l - 1];
+    const LevelGeom& D = P.plan.L[l];
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= D.w || y >= D.h) return;
+    const int4 cx = *reinterpret_cast<const int4*>(P.buf.coef32 + D.l32_x + 4 * x);
+    const int4 cy = *reinterpret_cast<const int4*>(P.buf.coef32 + D.l32_y + 4 * y);
+    const uint8_t* src = level_ptr(P, f, l - 1);
+    const int sp = level_pitch(P, l - 1);
+    const uint8_t* s0 = src + (int64_t)cy.x * sp;
+    const uint8_t* s1 = src + (int64_t)cy.y * sp;
+    const int a0 = cx.z & 0xFFFF, a1 = cx.z >> 16, b0 = cy.z & 0xFFFF, b1 = cy.z >> 16;
+    const int h0 = s0[cx.x] * a0 + s0[cx.y] * a1;
+    const int h1 = s1[cx.x] * a0 + s1[cx.y] * a1;
+    int v;
+    if (x < D.l32_xs)  // VResizeLinearVec_32s8u: _mm_mulhi_epi16 on h >> 4, then (t + 2) >> 2
+        v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+    else               // FixedPtCast<int, uchar, 22>
+        v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+    uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
+    dst[(int64_t)y * D.pitch + x] = (uint8_t)min(255, max(0, v));
+}
+
+// ------------------------------------------------------------------------
 // GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) with the 8-bit kernel
-// {18,34,49,55,49,34,18}: (sum over the 49 taps + 2^15) >> 16, saturated.
+// {18,34,49,55,49,34,18} over the 49 taps, sum / 2^16 rounded as OpenCV's
+// column filter does (oracle/orb.cpp gaussian_blur7): half to even in every
+// column up to the last multiple of 4 (its vector op: exact float sum, then
+// cvtps2dq), half up, (sum + 2^15) >> 16, in the last w % 4 columns (the
+// scalar FixedPtCastEx); saturated.  Half to even is (s + bit16(s)) >> 16
+// with s = sum + 2^15 - 1: the two differ only at a tie above an odd value.
 // Vertical first, in packed 16-bit lanes: a column sum of 7 bytes is at most
 // 255 * 257 = 65535, so each lane keeps its 4 columns as two u16 pairs and
 // forms the vertical sums with v_pk_mad_u16 over a rolling 7-row window (one
@@ -299,6 +339,9 @@ template <bool kInside, bool kSmall>
 __device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int sp, uint8_t* __restrict__ dst,
                                           int dp, int w, int h, int yw, int x0, bool store, int col_base,
                                           uint32_t col_sel) {
+    // the lane's 4 columns are all below w & ~3 (half to even) or all in the w % 4 tail (half up)
+    const uint32_t he = x0 + 4 <= w ? 1u : 0u;
+    const uint32_t R = he ? 0x7FFFu : 0x8000u;
     const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
     // all input rows are loaded up front (rows past the bottom are read, reflected, but not stored)
     uint32_t wds[kBlurR + 6];
@@ -334,7 +377,6 @@ __device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int s
         const uint32_t A = __builtin_bit_cast(uint32_t, a), B = __builtin_bit_cast(uint32_t, b);
         const u16x2 al = as_u16x2(dpp_from_left(A)), bl = as_u16x2(dpp_from_left(B));
         const u16x2 ar = as_u16x2(dpp_from_right(A)), br = as_u16x2(dpp_from_right(B));
-        constexpr uint32_t R = 1u << 15;
         uint32_t s0 = __builtin_amdgcn_udot2(al, (u16x2){0, 18}, R, false);
         s0 = __builtin_amdgcn_udot2(bl, (u16x2){34, 49}, s0, false);
         s0 = __builtin_amdgcn_udot2(a, (u16x2){55, 49}, s0, false);
@@ -351,6 +393,10 @@ __device__ __forceinline__ void blur_wave(const uint8_t* __restrict__ src, int s
         s3 = __builtin_amdgcn_udot2(b, (u16x2){49, 55}, s3, false);
         s3 = __builtin_amdgcn_udot2(ar, (u16x2){49, 34}, s3, false);
         s3 = __builtin_amdgcn_udot2(br, (u16x2){18, 0}, s3, false);
+        s0 += __builtin_amdgcn_ubfe(s0, 16, he);
+        s1 += __builtin_amdgcn_ubfe(s1, 16, he);
+        s2 += __builtin_amdgcn_ubfe(s2, 16, he);
+        s3 += __builtin_amdgcn_ubfe(s3, 16, he);
         // byte 2 of min(s, 2^24 - 1) == min(s >> 16, 255)
         s0 = min(s0, 0xFFFFFFu);
         s1 = min(s1, 0xFFFFFFu);
@@ -992,11 +1038,14 @@ __device__ void move_median_to_first(const A& a, int result, int x, int y, int z
 
 // Returns the retained size; the first `result` entries hold the kept
 // elements in libstdc++ order.  Must be called by the whole block.
+// semantics kOcv32: OpenCV 3.2's retainBest ran nth_element at begin + n (not
+// n - 1) and still read the boundary response at n - 1 (oracle retain_best).
 template <class A>
-__device__ int retain_best_block(const A& a, int n, int npoints, int depth, int32_t* Lpos, int32_t* Rasc, int* lds) {
+__device__ int retain_best_block(const A& a, int n, int npoints, int depth, int32_t* Lpos, int32_t* Rasc, int* lds,
+                                 int semantics = kOcv4) {
     if (npoints < 0 || n <= npoints) return n;
     if (npoints == 0) return 0;
-    const int nth = npoints - 1;
+    const int nth = semantics == kOcv32 ? npoints : npoints - 1;
     int first = 0, last = n;
     if (depth < 0) depth = 2 * (31 - __clz(n));
     bool heap_done = false;
@@ -1021,7 +1070,7 @@ __device__ int retain_best_block(const A& a, int n, int npoints, int depth, int3
     if (!heap_done && threadIdx.x == 0) insertion_sort(a, first, last);
     __syncthreads();
     // std::partition(begin+npoints, end, response >= ambiguous) (bidirectional)
-    auto amb = a.val(nth);
+    auto amb = a.val(npoints - 1);
     int nL = 0, nR = 0;
     for (int base = npoints; base < n; base += blockDim.x) {
         const int i = base + threadIdx.x;
@@ -1154,14 +1203,14 @@ __global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
         if (n <= kSelLdsCap) {
             for (int i = threadIdx.x; i < n; i += NT) s_key[i] = A[i];
             __syncthreads();
-            k = retain_best_block(FastKeys{s_key}, n, 2 * G.nper, -1, s_L, s_R, lds);
+            k = retain_best_block(FastKeys{s_key}, n, 2 * G.nper, -1, s_L, s_R, lds, P.plan.semantics);
             __syncthreads();
             for (int i = threadIdx.x; i < k; i += NT) A[i] = s_key[i];
         } else {
-            k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+            k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds, P.plan.semantics);
         }
     } else {
-        k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds);
+        k = retain_best_block(FastKeys{A}, n, 2 * G.nper, -1, Lpos, Rasc, lds, P.plan.semantics);
     }
     if (threadIdx.x == 0) P.buf.cnt1[f * kMaxLevels + l] = k;
 }
@@ -1280,17 +1329,17 @@ __global__ __launch_bounds__(NT) void select_harris_kernel(StreamParams P) {
                 s_key[i] = A[i];
             }
             __syncthreads();
-            k = retain_best_block(HarrisVals{s_v, s_key}, n, G.nper, -1, s_L, s_R, lds);
+            k = retain_best_block(HarrisVals{s_v, s_key}, n, G.nper, -1, s_L, s_R, lds, P.plan.semantics);
             __syncthreads();
             for (int i = threadIdx.x; i < k; i += NT) {
                 R[i] = s_v[i];
                 A[i] = s_key[i];
             }
         } else {
-            k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+            k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds, P.plan.semantics);
         }
     } else {
-        k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds);
+        k = retain_best_block(HarrisVals{R, A}, n, G.nper, -1, Lpos, Rasc, lds, P.plan.semantics);
     }
     if (threadIdx.x == 0) P.buf.cnt2[f * kMaxLevels + l] = k;
 }
@@ -1521,9 +1570,9 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 }
 
 __global__ void test_retain_best_kernel(float* resp, uint32_t* payload, int32_t* tmp, int n, int npoints, int depth,
-                                        int* kout) {
+                                        int semantics, int* kout) {
     __shared__ int lds[64];
-    int k = retain_best_block(HarrisVals{resp, payload}, n, npoints, depth, tmp, tmp + n + 1, lds);
+    int k = retain_best_block(HarrisVals{resp, payload}, n, npoints, depth, tmp, tmp + n + 1, lds, semantics);
     if (threadIdx.x == 0) *kout = k;
 }
 
@@ -1534,6 +1583,11 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const int F = P.nframes;
     mark(ev, 0, 0, s);
     for (int l = 1; l < pl.nlevels; ++l) {
+        if (pl.semantics == kOcv32) {
+            hipLaunchKernelGGL(resize_level_ocv32_kernel, dim3((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F),
+                               dim3(256), 0, s, P, l);
+            continue;
+        }
         // staged tile fits when both ratios are <= 1.25: 256 * 1.25 + 12 bytes <= kRsW words,
         // 32 * 1.25 + 2 rows <= kRsRows
         const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
@@ -1574,9 +1628,9 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
 }
 
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
-                                   int* d_k, hipStream_t s) {
+                                   int semantics, int* d_k, hipStream_t s) {
     hipLaunchKernelGGL(test_retain_best_kernel, dim3(1), dim3(kSelNT), 0, s, d_resp, d_payload, d_tmp, n, n_points,
-                       depth, d_k);
+                       depth, semantics, d_k);
     return hipGetLastError();
 }
 

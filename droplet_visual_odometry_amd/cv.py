@@ -21,12 +21,22 @@ on each.
 """
 from __future__ import annotations
 
+import os
 from collections.abc import Sequence
 
 import numpy as np
 
 from . import ops
-from ._native import DVOError
+from ._native import DVOError, opencv_semantics
+
+# Which OpenCV release's semantics the cv2 stand-ins reproduce (include/dvo.h
+# DVO_OPENCV_*): "4.x" by default, or "3.2" -- the version the reference most
+# likely ran (ROS Melodic, Python 2.7): ORB's INTER_LINEAR
+# pyramid and retainBest, and BFMatcher's 3.x cross check.  Set
+# DVO_OPENCV_SEMANTICS=3.2 in the environment (read at import), or assign
+# cv.OPENCV_SEMANTICS before creating the detector / matcher.
+OPENCV_SEMANTICS = os.environ.get("DVO_OPENCV_SEMANTICS", "4.x")
+opencv_semantics(OPENCV_SEMANTICS)  # validate
 
 # cv2 constants used by the reference
 NORM_L1 = 2
@@ -185,6 +195,7 @@ class ORB:
             raise error("only the cv.ORB_create() defaults (other than nfeatures/fastThreshold) are implemented")
         self.nfeatures = int(nfeatures)
         self.fastThreshold = int(fastThreshold)
+        self.opencv = OPENCV_SEMANTICS
 
     def getMaxFeatures(self):
         return self.nfeatures
@@ -199,7 +210,7 @@ class ORB:
             raise error("useProvidedKeypoints is not supported")
         img = _gray(image)
         try:
-            kps, desc = ops.detect_and_compute(img, self.nfeatures, self.fastThreshold)
+            kps, desc = ops.detect_and_compute(img, self.nfeatures, self.fastThreshold, self.opencv)
         except DVOError as e:
             raise error(str(e)) from e
         return KeyPoints(kps), (desc if len(kps) else None)
@@ -249,13 +260,15 @@ class BFMatcher:
     on float descriptors (the SIFT/SURF branches, v3:99-106).
 
     crossCheck follows OpenCV 4.x (mutual nearest neighbour) unless
-    legacy_crosscheck=True selects OpenCV 3.x's reverse-pass semantics; it is
-    implemented for NORM_HAMMING (the reference sets it only there)."""
+    legacy_crosscheck=True (default: OPENCV_SEMANTICS == "3.2") selects OpenCV
+    3.x's reverse-pass semantics; it is implemented for NORM_HAMMING (the
+    reference sets it only there)."""
 
-    def __init__(self, normType=NORM_L2, crossCheck=False, legacy_crosscheck=False):
+    def __init__(self, normType=NORM_L2, crossCheck=False, legacy_crosscheck=None):
         self.normType = normType
         self.crossCheck = bool(crossCheck)
-        self.legacy_crosscheck = bool(legacy_crosscheck)
+        self.legacy_crosscheck = (opencv_semantics(OPENCV_SEMANTICS) == 1 if legacy_crosscheck is None
+                                  else bool(legacy_crosscheck))
 
     def _check_l1(self):
         if self.normType != NORM_L1:

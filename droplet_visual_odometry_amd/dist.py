@@ -5,24 +5,23 @@ E -> R, t depends only on its two frames; visual_odometry_v3.py:384-408).  The
 pairs are split into contiguous per-rank runs; a rank processing pairs
 [p0, p1) needs frames [p0, p1] (a one-frame halo on the right, shared with the
 next rank, detected twice — the only redundant work).  No data-path
-collective: after the batch each rank holds its 256-byte pair records and the
-only exchange is one all-gather of those records (RCCL over xGMI on the GPU,
-gloo in the CPU tests) to reassemble the pose stream in order.
+collective: after the batch each rank holds its 256-byte pair records.
 
-The marker-scale step of pair p needs the previous pair's projection matrix
-P = K [R | t] (v3:264-265, :344).  So a rank whose run starts at p0 > 0 also
-loads frame p0-1 (the left halo, `shard_window`) and computes pair p0-1: its
-R|t is P_prev for p0, exactly as on one rank, and its record and T_rel are
-dropped before the exchange.  (On one rank P_prev is the last *successful*
-pair's; the halo reproduces that whenever the halo pair itself succeeds, i.e.
-unless frame p0-1 or p0 has no features.)
+Two things couple adjacent pairs, both cheap and both downstream of the
+records: the marker-scale step of pair p triangulates against the previous
+*successful* pair's projection P = K [R | t] (v3:264-265, :344), and the
+absolute pose is the prefix product T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367).
+So the exchange is one all-gather of each rank's records plus the marker
+corners of its pairs (`ShardedPoseStream`), and rank 0 runs the whole pose
+tail over the window in pair order from the gathered records
+(`stream.PoseTail` -> dvo_pose_tail_records: the same kernels and the same
+record fields as the single-rank dvo_stream_pose_tail).  P_prev of a rank's
+first pair is then the last successful pair's wherever it was computed —
+including when the pairs at a shard boundary fail — so records, T_rel and
+T_abs are bit-identical to one rank processing the whole stream.
 
-`ShardedPoseStream.exchange` all-gathers every rank's records and T_rel rows in
-pair order; rank 0 then chains T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) over
-the whole window on the device (`stream.PoseChain`, the same left-to-right
-4x4 arithmetic as the single-rank pose tail, so T_abs is bit-identical).  The
-host helpers `local_chain` / `compose_chain` fold per-rank partial products
-instead (equal up to reassociation, tests/test_dist.py).
+The host helpers `local_chain` / `compose_chain` fold per-rank partial
+products instead (equal up to reassociation, tests/test_dist.py).
 """
 from __future__ import annotations
 
@@ -39,13 +38,12 @@ def shard_pairs(n_frames: int, world: int, rank: int) -> tuple[int, int]:
     return p0, p0 + base + (1 if rank < extra else 0)
 
 
-def shard_frames(n_frames: int, world: int, rank: int, left_halo: bool = False) -> tuple[int, int]:
-    """Frame range [f0, f1) a rank must load for its pairs (right halo included;
-    with left_halo also the frame before its first pair, when there is one)."""
+def shard_frames(n_frames: int, world: int, rank: int) -> tuple[int, int]:
+    """Frame range [f0, f1) a rank must load for its pairs (right halo included)."""
     p0, p1 = shard_pairs(n_frames, world, rank)
     if p1 <= p0:
         return p0, p0
-    return (p0 - 1 if left_halo and p0 > 0 else p0), p1 + 1
+    return p0, p1 + 1
 
 
 def max_pairs_per_rank(n_frames: int, world: int) -> int:
@@ -54,62 +52,160 @@ def max_pairs_per_rank(n_frames: int, world: int) -> int:
 
 def shard_window(n_pairs: int, world: int, rank: int, first_pair: int = 0):
     """`rank`'s share of a window of `n_pairs` consecutive pairs of ONE stream
-    starting at global pair `first_pair`: (p0, p1, f0, f1, halo) -- pairs
-    [p0, p1), frames [f0, f1) to load (pair p is frames p, p+1) and halo = 1
-    when frame p0-1 is loaded too, so that the rank's first computed pair is
-    the dropped halo pair p0-1."""
+    starting at global pair `first_pair`: (p0, p1, f0, f1) -- pairs [p0, p1)
+    and the frames [f0, f1) = [p0, p1 + 1) to load (pair p is frames p, p+1)."""
     a, b = shard_pairs(n_pairs + 1, world, rank)
     p0, p1 = first_pair + a, first_pair + b
     if p1 <= p0:
-        return p0, p0, p0, p0, 0
-    halo = 1 if p0 > 0 else 0
-    return p0, p1, p0 - halo, p1 + 1, halo
+        return p0, p0, p0, p0
+    return p0, p1, p0, p1 + 1
 
 
 class ShardedPoseStream:
     """The exchange step of one pose stream sharded across ranks (SURVEY.md
     §8e, BASELINE configs[3]): windows of `window_pairs` pairs, each rank
-    computing its `shard_window` run (halo pair first) on its own GPU.
+    computing its `shard_window` run on its own GPU.
 
-    `exchange(records, T_rel, halo)` takes the rank's computed records
-    (uint8, 256 B per pair, halo pair first) and T_rel ([pairs, 4, 4] float64)
-    and returns the window's records and T_rel in global pair order on every
-    rank: one all-gather each (RCCL over xGMI; gloo through host memory with
-    host_gather=True).  Inputs are sliced in place, so the gathered sends are
-    the rank's buffers themselves: they must hold at least halo + cap pairs,
-    cap = max pairs per rank.  The returned tensors are views of the receive
-    buffers (no copy when the shards are equal), valid until the next exchange."""
+    One send buffer per instance holds the rank's records (`records`, where
+    FrameStream.process writes them: capacity `cap` pairs) followed by its
+    pairs' marker corners (`set_corners`: previous-frame and current-frame
+    corners, k x 2 doubles each, as the harness passes them to
+    visual_odometry_calculations, trajectory_evaluation_dual_process.py:158-164).
+    `exchange()` all-gathers the send buffers in one collective (RCCL over
+    xGMI; gloo through host memory with host_gather=True) and returns the
+    window's records, previous and current corners in global pair order as
+    new contiguous tensors on `device`.
 
-    def __init__(self, world: int, rank: int, window_pairs: int, device, group=None, host_gather: bool = False):
+    Ordering contract (RCCL): the collective runs on torch's current stream.
+    Before it, that stream must wait for the library stream that wrote
+    `records`; before the next write into `records`, the library stream must
+    wait for `exchange`'s `done` event (bench.py main_sharded)."""
+
+    def __init__(self, world: int, rank: int, window_pairs: int, device, k: int = 4, group=None,
+                 host_gather: bool = False):
         import torch
         from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
-        self.world, self.rank, self.window_pairs, self.group = world, rank, window_pairs, group
+        self.world, self.rank, self.window_pairs, self.group, self.k = world, rank, window_pairs, group, k
+        self.device = torch.device(device)
         self.rb = PAIR_RECORD_DTYPE.itemsize
+        self.cb = k * 2 * 8                       # one frame's corners
         self.counts = [b - a for a, b in (shard_pairs(window_pairs + 1, world, r) for r in range(world))]
         self.cap = max(self.counts)
         self.n_local = self.counts[rank]
+        self.seg = self.cap * (self.rb + 2 * self.cb)
         self.host_gather = host_gather
-        gdev = torch.device("cpu") if host_gather else torch.device(device)
-        self.recv_rec = torch.empty(world * self.cap * self.rb, dtype=torch.uint8, device=gdev)
-        self.recv_T = torch.empty((world * self.cap, 4, 4), dtype=torch.float64, device=gdev)
+        self.send = torch.zeros(self.seg, dtype=torch.uint8, device=self.device)
+        gdev = torch.device("cpu") if host_gather else self.device
+        self.recv = torch.empty(world * self.seg, dtype=torch.uint8, device=gdev)
+        self.done = None  # torch.cuda.Event recorded after the last collective (device gathers)
 
-    def exchange(self, records, T_rel, halo: int):
-        import torch.distributed as dist
-        rb, cap = self.rb, self.cap
-        if records.numel() < (halo + cap) * rb or T_rel.shape[0] < halo + cap:
-            raise ValueError(f"buffers must hold halo + {cap} pairs")
-        send_rec = records[halo * rb:(halo + cap) * rb]
-        send_T = T_rel[halo:halo + cap]
-        if self.host_gather:
-            send_rec, send_T = send_rec.cpu(), send_T.cpu()
-        dist.all_gather_into_tensor(self.recv_rec, send_rec, group=self.group)
-        dist.all_gather_into_tensor(self.recv_T.view(-1), send_T.reshape(-1), group=self.group)
-        if all(c == cap for c in self.counts):
-            return self.recv_rec, self.recv_T
+    @property
+    def records(self):
+        """The rank's record slots (uint8, cap x 256 B) inside the send buffer."""
+        return self.send[:self.cap * self.rb]
+
+    def _corner_block(self, which: int):
+        o = self.cap * self.rb + which * self.cap * self.cb
+        return self.send[o:o + self.cap * self.cb].view(__import__("torch").float64).view(self.cap, self.k, 2)
+
+    def set_corners(self, c_prev, c_cur):
+        """Copy the rank's per-pair corners ([n_local, k, 2] float64) into the
+        send buffer (on torch's current stream)."""
+        n = self.n_local
+        if tuple(c_prev.shape) != (n, self.k, 2) or tuple(c_cur.shape) != (n, self.k, 2):
+            raise ValueError(f"corners must be [{n}, {self.k}, 2]")
+        self._corner_block(0)[:n].copy_(c_prev, non_blocking=True)
+        self._corner_block(1)[:n].copy_(c_cur, non_blocking=True)
+
+    def exchange(self):
         import torch
-        recs = torch.cat([self.recv_rec[r * cap * rb:(r * cap + c) * rb] for r, c in enumerate(self.counts)])
-        Ts = torch.cat([self.recv_T[r * cap:r * cap + c] for r, c in enumerate(self.counts)])
-        return recs, Ts
+        import torch.distributed as dist
+        send = self.send.cpu() if self.host_gather else self.send
+        dist.all_gather_into_tensor(self.recv, send, group=self.group)
+        if not self.host_gather and self.recv.is_cuda:
+            self.done = torch.cuda.Event()
+            self.done.record(torch.cuda.current_stream(self.recv.device))
+        v = self.recv.view(self.world, self.seg)
+        rb, cb, cap = self.rb, self.cb, self.cap
+        recs = torch.cat([v[r, :c * rb] for r, c in enumerate(self.counts)])
+        cp = torch.cat([v[r, cap * rb:cap * rb + c * cb] for r, c in enumerate(self.counts)])
+        cc = torch.cat([v[r, cap * (rb + cb):cap * (rb + cb) + c * cb] for r, c in enumerate(self.counts)])
+        n = self.window_pairs
+        cp = cp.view(torch.float64).view(n, self.k, 2)
+        cc = cc.view(torch.float64).view(n, self.k, 2)
+        if self.host_gather:
+            recs, cp, cc = (x.to(self.device) for x in (recs, cp, cc))
+        return recs, cp, cc
+
+
+class ShardedStreamRunner:
+    """One rank's loop over a sharded pose stream (bench.py main_sharded and
+    tests/test_gpu_sharded.py run this same code): `streams` windows in flight,
+    each on its own FrameStream / HIP stream and its own ShardedPoseStream
+    send buffer, and on rank 0 one PoseTail whose carry continues across
+    windows.
+
+    `step(frames, c_prev, c_cur)` enqueues one window: frames = the rank's
+    n_local + 1 device frames, c_prev / c_cur its n_local pairs' corners.
+    Returns (records, T_rel, T_abs): the window's gathered records (every
+    rank) and rank 0's relative / absolute poses (None elsewhere), valid until
+    the same slot is reused `streams` steps later.
+
+    Ordering without host syncs on the device-gather path: the library stream
+    waits for the slot's previous collective before writing its records;
+    torch's stream waits for the records before the collective; rank 0's tail
+    runs after the collective on torch's stream (ordered_side_stream)."""
+
+    def __init__(self, width: int, height: int, K, nfeatures: int, window_pairs: int, world: int, rank: int,
+                 marker_length: float, ctx=None, device=None, max_iters: int = 1000, streams: int = 2, k: int = 4,
+                 host_gather: bool = False, group=None):
+        import torch
+        from droplet_visual_odometry_amd._native import Context
+        from droplet_visual_odometry_amd.stream import FrameStream, PoseTail
+        self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
+        dev = torch.device("cuda", self.ctx.device)
+        self.S, self.rank, self.host_gather = max(1, streams), rank, host_gather
+        self.shs = [ShardedPoseStream(world, rank, window_pairs, dev, k=k, group=group, host_gather=host_gather)
+                    for _ in range(self.S)]
+        self.n_local = self.shs[0].n_local
+        self.fss = [FrameStream(width, height, K, nfeatures=nfeatures, max_frames=self.n_local + 1,
+                                max_iters=max_iters, ctx=self.ctx) for _ in range(self.S)]
+        self.tail = PoseTail(K, marker_length, ctx=self.ctx) if rank == 0 else None
+        self.T_rel = [torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev) for _ in range(self.S)] \
+            if rank == 0 else None
+        self.T_abs = [torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev) for _ in range(self.S)] \
+            if rank == 0 else None
+        self.i = 0
+
+    def step(self, frames, c_prev, c_cur):
+        import torch
+        k = self.i % self.S
+        self.i += 1
+        fs, sh = self.fss[k], self.shs[k]
+        if frames.shape[0] != self.n_local + 1:
+            raise ValueError(f"rank {self.rank} needs {self.n_local + 1} frames per window")
+        fs.wait_event(sh.done)  # the slot's previous collective has read its send buffer
+        fs.process(frames, sh.records, wait_torch=False)
+        if self.host_gather:
+            fs.sync()
+        else:
+            torch.cuda.current_stream(fs.device).wait_event(fs.record_event())
+        sh.set_corners(c_prev, c_cur)
+        recs, cp, cc = sh.exchange()
+        if self.tail is None:
+            return recs, None, None
+        T_rel, T_abs = self.tail.run(recs, cp, cc, self.T_rel[k], self.T_abs[k])
+        return recs, T_rel, T_abs
+
+    def sync(self):
+        import torch
+        for f in self.fss:
+            f.sync()
+        torch.cuda.synchronize()
+
+    def close(self):
+        for f in self.fss:
+            f.close()
 
 
 def gather_records(records, n_local: int, n_frames: int, group=None):

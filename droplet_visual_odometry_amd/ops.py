@@ -28,14 +28,15 @@ def _ctx(ctx):
     return ctx if ctx is not None else Context.default()
 
 
-def detect_and_compute(img: np.ndarray, nfeatures: int = 500, fast_threshold: int = 20, ctx=None):
-    """ORB keypoints (structured KEYPOINT_DTYPE array) and uint8[N, 32] descriptors."""
+def detect_and_compute(img: np.ndarray, nfeatures: int = 500, fast_threshold: int = 20, opencv="4.x", ctx=None):
+    """ORB keypoints (structured KEYPOINT_DTYPE array) and uint8[N, 32] descriptors.
+    opencv: "4.x" (default) or "3.2" semantics (include/dvo.h DVO_OPENCV_*)."""
     c = _ctx(ctx)
     img = np.ascontiguousarray(img)
     if img.dtype != np.uint8 or img.ndim != 2:
         raise DVOError(-1, "detect_and_compute expects a mono8 image (uint8[H, W])")
     h, w = img.shape
-    prm = orb_params(nfeatures=nfeatures, fast_threshold=fast_threshold)
+    prm = orb_params(nfeatures=nfeatures, fast_threshold=fast_threshold, opencv=opencv)
     cap = nfeatures + 512
     while True:
         kps = np.zeros(cap, KEYPOINT_DTYPE)
@@ -184,13 +185,14 @@ def triangulate_points(P1, P2, x1, x2, ctx=None) -> np.ndarray:
 
 
 # ---- device test hooks --------------------------------------------------------
-def test_retain_best(resp, n_points, depth=-1, ctx=None):
+def test_retain_best(resp, n_points, depth=-1, opencv="4.x", ctx=None):
+    from ._native import opencv_semantics
     c = _ctx(ctx)
     resp = np.ascontiguousarray(resp, np.float32)
     perm = np.zeros(max(len(resp), 1), np.int32)
     k = ctypes.c_int()
-    c.check(c.lib.dvo_test_retain_best(c.h, ptr(resp), len(resp), int(n_points), int(depth), ptr(perm),
-                                       ctypes.byref(k)))
+    c.check(c.lib.dvo_test_retain_best(c.h, ptr(resp), len(resp), int(n_points), int(depth),
+                                       opencv_semantics(opencv), ptr(perm), ctypes.byref(k)))
     return perm[:k.value].copy()
 
 

@@ -21,15 +21,22 @@ from ._native import (DMATCH_DTYPE, KEYPOINT_DTYPE, PAIR_RECORD_DTYPE, Context, 
 
 class FrameStream:
     def __init__(self, width: int, height: int, K, nfeatures: int = 500, max_frames: int = 64, prob: float = 0.999,
-                 threshold: float = 1.0, max_iters: int = 1000, cross_check: int = 1, dist_thresh: float = 50.0,
-                 device: int | None = None, ctx: Context | None = None):
+                 threshold: float = 1.0, max_iters: int = 1000, cross_check: int | None = None,
+                 dist_thresh: float = 50.0, device: int | None = None, ctx: Context | None = None, opencv="4.x"):
+        """opencv: the OpenCV version whose semantics the path reproduces, "4.x"
+        (default) or "3.2" (ORB pyramid / retainBest, and cross_check defaults
+        to the 3.x reverse pass); see include/dvo.h DVO_OPENCV_*."""
+        from ._native import opencv_semantics
+        sem = opencv_semantics(opencv)
+        if cross_check is None:
+            cross_check = 2 if sem == 1 else 1
         if ctx is not None and device is not None and device != ctx.device:
             raise ValueError(f"device {device} != context device {ctx.device}")
         self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
         self.device = torch.device("cuda", self.ctx.device)  # the library runs on the context's device
         cfg = StreamConfig()
         cfg.width, cfg.height, cfg.max_frames = int(width), int(height), int(max_frames)
-        cfg.orb = orb_params(nfeatures=nfeatures)
+        cfg.orb = orb_params(nfeatures=nfeatures, opencv=opencv)
         K = np.asarray(K, np.float64).reshape(9)
         for i in range(9):
             cfg.K[i] = float(K[i])
@@ -100,6 +107,12 @@ class FrameStream:
         ev = torch.cuda.Event()
         ev.record(self._ext)
         return ev
+
+    def wait_event(self, ev):
+        """Order the library's HIP stream after a torch.cuda.Event (e.g. the
+        all-gather that last read this stream's records buffer)."""
+        if ev is not None:
+            self._ext.wait_event(ev)
 
     def share_pose(self, owner: "FrameStream"):
         """Chain this stream's pose tails on `owner`'s carry (batches alternating
@@ -237,3 +250,58 @@ class PoseChain:
                                                        T_abs.data_ptr(), st))
         return T_abs
 
+
+
+class PoseTail:
+    """Pose tail over pair records (dvo_pose_tail_records): the marker-scaled
+    relative poses (v3:309-345) and the absolute chain (v3:367) for records
+    that arrive from elsewhere -- the reassembly step of a sharded pose stream
+    (dist.ShardedPoseStream), run by rank 0 over the whole window in pair order.
+    Same kernels and record fields as FrameStream.pose_tail, so the result is
+    bit-identical to one rank's stream.  The carry (P_prev | T_abs) persists
+    across calls on the device.  Runs on torch's current stream, where the
+    all-gather that produced the records ran (ordered_side_stream)."""
+
+    def __init__(self, K, marker_length: float, ctx: Context | None = None, device: int | None = None):
+        self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
+        self.device = torch.device("cuda", self.ctx.device)
+        self.K = np.ascontiguousarray(np.asarray(K, np.float64).reshape(3, 3))
+        self.marker_length = float(marker_length)
+        self.carry = torch.empty(28, dtype=torch.float64, device=self.device)
+        self.reset()
+
+    def reset(self, P0=None, T0=None):
+        """P_prev (3x4, default K[I|0] as in controlled mode, v3:164-166) and the
+        absolute pose (4x4, default identity) before the next record."""
+        P0 = self.K @ np.hstack((np.eye(3), np.zeros((3, 1)))) if P0 is None else np.asarray(P0, np.float64)
+        T0 = np.eye(4) if T0 is None else np.asarray(T0, np.float64)
+        c = np.concatenate([np.asarray(P0, np.float64).reshape(12), np.asarray(T0, np.float64).reshape(16)])
+        self.carry.copy_(torch.from_numpy(c))
+
+    def run(self, records: torch.Tensor, corners_prev: torch.Tensor, corners_cur: torch.Tensor,
+            T_rel: torch.Tensor | None = None, T_abs: torch.Tensor | None = None):
+        """records: uint8 device tensor of n x 256 B; corners: float64 [n, k, 2]
+        device tensors.  Returns (T_rel, T_abs) [n, 4, 4]."""
+        rb = PAIR_RECORD_DTYPE.itemsize
+        if records.dtype != torch.uint8 or not records.is_cuda or not records.is_contiguous() or records.numel() % rb:
+            raise ValueError("records must be a contiguous uint8 device tensor of whole 256-B records")
+        n = records.numel() // rb
+        for c in (corners_prev, corners_cur):
+            if c.dtype != torch.float64 or not c.is_cuda or not c.is_contiguous() or c.dim() != 3 \
+                    or c.shape[0] != n or c.shape[2] != 2:
+                raise ValueError(f"corners must be contiguous float64 [{n}, k, 2] device tensors")
+        k = corners_prev.shape[1]
+        if corners_cur.shape[1] != k:
+            raise ValueError("previous and current corners differ in k")
+        if T_rel is None:
+            T_rel = torch.empty((n, 4, 4), dtype=torch.float64, device=self.device)
+        if T_abs is None:
+            T_abs = torch.empty((n, 4, 4), dtype=torch.float64, device=self.device)
+        for T in (T_rel, T_abs):
+            if T.dtype != torch.float64 or not T.is_contiguous() or T.shape[0] < n:
+                raise ValueError(f"T_rel / T_abs must be contiguous float64 [>= {n}, 4, 4] device tensors")
+        with ordered_side_stream(self.device) as st:
+            self.ctx.check(self.ctx.lib.dvo_pose_tail_records(
+                self.ctx.h, records.data_ptr(), n, ptr(self.K), corners_prev.data_ptr(), corners_cur.data_ptr(), k,
+                self.marker_length, self.carry.data_ptr(), T_rel.data_ptr(), T_abs.data_ptr(), st))
+        return T_rel, T_abs

@@ -44,6 +44,15 @@ typedef struct {
     float distance;
 } dvo_dmatch;
 
+/* OpenCV version whose ORB / BFMatcher semantics the path reproduces.  The
+ * reference pins none (package.xml:21-30); its Python 2.7 .pyc files and ROS
+ * Melodic docs point at OpenCV 3.2.  4.x is the default.
+ * DVO_OPENCV_32: the pyramid is resize(INTER_LINEAR) with 11-bit weights and
+ * the SSE2 vertical pass (4.x: INTER_LINEAR_EXACT), and retainBest runs
+ * nth_element at n instead of n - 1; everything else is common to both. */
+#define DVO_OPENCV_4X 0
+#define DVO_OPENCV_32 1
+
 /* cv.ORB_create() parameters (visual_odometry_v3.py:96 uses the defaults).
  * Only the defaults other than nfeatures are implemented; others -> DVO_EINVAL. */
 typedef struct {
@@ -56,6 +65,7 @@ typedef struct {
     int32_t score_type;     /* 0 = HARRIS_SCORE */
     int32_t patch_size;     /* 31    */
     int32_t fast_threshold; /* 20    */
+    int32_t opencv_semantics; /* DVO_OPENCV_4X (0) or DVO_OPENCV_32 */
 } dvo_orb_params;
 
 int dvo_version(void);
@@ -203,7 +213,8 @@ int dvo_stream_process_undistorted(dvo_stream* s, dvo_undistort* u, const uint8_
 void* dvo_stream_hip_stream(dvo_stream* s);
 /* Pose tail of get_transformation_between_two_frames (v3:309-345) and
  * previous_current_matching (v3:367) for the pairs of the last
- * dvo_stream_process, on the device:
+ * dvo_stream_process (read from that call's d_records, which must stay
+ * allocated until the tail has run), on the device:
  *   P_cur = K [R | t];  X = triangulatePoints(P_prev, P_cur, c_prev, c_cur);
  *   d = |X[:3,0] - X[:3,1]| (homogeneous, not divided by W: D3);  s = L / d;
  *   T_rel = translation_matrix(t s) . euler_matrix(euler_from_matrix(R,'rxyz'),'sxyz');
@@ -218,6 +229,23 @@ int dvo_stream_reset_pose(dvo_stream* s, const double* P0 /* host 12 */, const d
 int dvo_stream_share_pose(dvo_stream* s, dvo_stream* owner);
 int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
                          double marker_length, double* d_T_rel, double* d_T_abs);
+
+/* The same pose tail over caller-supplied pair records: the reassembly step of
+ * one pose stream sharded across ranks.  Every rank computes
+ * the records of its run of pairs (dvo_stream_process), the ranks all-gather
+ * records and per-pair marker corners, and rank 0 runs this over the whole
+ * window in pair order.  The tail reads only R, t, status and n_models of each
+ * record (a pair counts as successful iff status == DVO_OK and n_models == 1,
+ * as in dvo_stream_pose_tail), so P_prev of the first pair of a run is the
+ * last successful pair's even when it lies on another rank: the result is
+ * bit-identical to one rank running dvo_stream_pose_tail over the stream.
+ * K: host 9 doubles.  d_carry: device 28 doubles, P_prev (3x4) | T_abs (4x4),
+ * the state before the first pair on entry and after the last on return
+ * (controlled mode: P0 = K [I | 0], v3:164-166).  Asynchronous on hip_stream
+ * (NULL = the context's stream). */
+int dvo_pose_tail_records(dvo_ctx* ctx, const dvo_pair_record* d_records, int pairs, const double* K,
+                          const double* d_corners_prev, const double* d_corners_cur, int k, double marker_length,
+                          double* d_carry, double* d_T_rel, double* d_T_abs, void* hip_stream);
 
 /* The absolute-pose chain of previous_current_matching (v3:367,
  * T_robot_cur = T_robot_prev . T_prev->cur) on its own, for pose streams
@@ -245,7 +273,8 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
 /* Test hooks: exercise one device algorithm in isolation. */
 /* KeyPointsFilter::retainBest permutation on `n` float responses (GPU emulation
  * of libstdc++ nth_element + partition); depth < 0 = libstdc++ default. */
-int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int32_t* perm, int* k_out);
+int dvo_test_retain_best(dvo_ctx* ctx, const float* resp, int n, int n_points, int depth, int semantics,
+                         int32_t* perm, int* k_out);
 /* RANSACUpdateNumIters on the device for a batch of (ep) values. */
 int dvo_test_update_num_iters(dvo_ctx* ctx, double p, const double* ep, int n, int model_points, int max_iters,
                               int32_t* out);

@@ -45,6 +45,16 @@ int ora_retain_best_depth(const float* resp, int n, int n_points, int depth, int
 int ora_orb_detect_and_compute(const uint8_t* img, int w, int h, int stride,
                                int nfeatures, ora_keypoint* kps, uint8_t* desc,
                                int cap, int* n_out);
+// The same with a choice of OpenCV semantics (the reference
+// most likely ran OpenCV 3.2): 0 = 4.x (INTER_LINEAR_EXACT pyramid, retainBest
+// nth at n-1; the default everywhere), 1 = 3.2 (INTER_LINEAR 11-bit pyramid with
+// the SSE2 vertical pass, retainBest nth at n).  The blur is the same in both.
+int ora_orb_detect_and_compute_v(const uint8_t* img, int w, int h, int stride, int nfeatures, int semantics,
+                                 ora_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+int ora_orb_pyramid_v(const uint8_t* img, int w, int h, int stride, int nlevels, int blurred, int semantics,
+                      uint8_t* out);
+int ora_retain_best_v(const float* resp, int n, int n_points, int semantics, int32_t* perm);
+int ora_retain_best_depth_v(const float* resp, int n, int n_points, int depth, int semantics, int32_t* perm);
 
 // ---- BFMatcher(NORM_HAMMING, crossCheck) ------------------------------------
 // mode 0: no cross check, 1: OpenCV 4.x mutual check, 2: OpenCV 3.x reverse-only.

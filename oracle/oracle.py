@@ -32,9 +32,13 @@ _d = ctypes.c_double
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(_LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+    """make the oracle library (incremental: rebuilt when a source changed)."""
+    subprocess.check_call(["make", "-s", "-C", _HERE] + (["-B"] if force else []))
     return _LIB_PATH
+
+
+# OpenCV semantics of the ORB restatement (oracle.h ora_orb_detect_and_compute_v)
+OCV4, OCV32 = 0, 1
 
 
 def host_cpu():
@@ -80,6 +84,10 @@ def lib():
             "ora_retain_best": [_f32p, _c, _c, _i32p],
             "ora_retain_best_depth": [_f32p, _c, _c, _c, _i32p],
             "ora_orb_detect_and_compute": [_u8p, _c, _c, _c, _c, _kpp, _u8p, _c, _ip],
+            "ora_orb_detect_and_compute_v": [_u8p, _c, _c, _c, _c, _c, _kpp, _u8p, _c, _ip],
+            "ora_orb_pyramid_v": [_u8p, _c, _c, _c, _c, _c, _c, _u8p],
+            "ora_retain_best_v": [_f32p, _c, _c, _c, _i32p],
+            "ora_retain_best_depth_v": [_f32p, _c, _c, _c, _c, _i32p],
             "ora_bf_match_hamming": [_u8p, _c, _u8p, _c, _c, _i32p, _i32p, _f32p, _ip],
             "ora_bf_knn_float": [_f32p, _c, _f32p, _c, _c, _c, _c, _i32p, _f32p],
             "ora_find_essential": [_f64p, _f64p, _c, _f64p, _d, _d, _c, _f64p, _ip, _u8p, _ip],
@@ -117,12 +125,12 @@ def features_per_level(nfeatures, nlevels=8):
     return out.tolist()
 
 
-def pyramid(img, nlevels=8, blurred=False):
+def pyramid(img, nlevels=8, blurred=False, semantics=OCV4):
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     sizes = level_sizes(w, h, nlevels)
     out = np.zeros(sum(a * b for a, b in sizes), np.uint8)
-    lib().ora_orb_pyramid(img, w, h, w, nlevels, int(blurred), out)
+    lib().ora_orb_pyramid_v(img, w, h, w, nlevels, int(blurred), int(semantics), out)
     levels, off = [], 0
     for lw, lh in sizes:
         levels.append(out[off:off + lw * lh].reshape(lh, lw))
@@ -141,24 +149,25 @@ def fast(img, threshold=20):
     return buf[:3 * n.value].reshape(-1, 3)
 
 
-def retain_best(resp, n_points, depth=None):
+def retain_best(resp, n_points, depth=None, semantics=OCV4):
     resp = np.ascontiguousarray(resp, np.float32)
     perm = np.zeros(max(len(resp), 1), np.int32)
     if depth is None:
-        k = lib().ora_retain_best(resp, len(resp), n_points, perm)
+        k = lib().ora_retain_best_v(resp, len(resp), n_points, int(semantics), perm)
     else:
-        k = lib().ora_retain_best_depth(resp, len(resp), n_points, depth, perm)
+        k = lib().ora_retain_best_depth_v(resp, len(resp), n_points, depth, int(semantics), perm)
     return perm[:k]
 
 
-def detect_and_compute(img, nfeatures=500):
+def detect_and_compute(img, nfeatures=500, semantics=OCV4):
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     cap = 4 * nfeatures + 1024
     kps = np.zeros(cap, KEYPOINT_DTYPE)
     desc = np.zeros((cap, 32), np.uint8)
     n = ctypes.c_int()
-    rc = lib().ora_orb_detect_and_compute(img, w, h, w, nfeatures, kps, desc, cap, ctypes.byref(n))
+    rc = lib().ora_orb_detect_and_compute_v(img, w, h, w, nfeatures, int(semantics), kps, desc, cap,
+                                            ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
 
@@ -319,13 +328,15 @@ def keypoints_to_points(kps):
     return np.stack([kps["x"], kps["y"]], axis=1).astype(np.float32)
 
 
-def pair_pose(img_prev, img_cur, K, nfeatures=500, max_iters=1000, kp_prev=None):
-    """The full per-pair hot path (v3:384-408 minus the host pose tail) on the CPU."""
+def pair_pose(img_prev, img_cur, K, nfeatures=500, max_iters=1000, kp_prev=None, semantics=OCV4):
+    """The full per-pair hot path (v3:384-408 minus the host pose tail) on the CPU.
+    semantics OCV32: OpenCV 3.2's ORB pyramid / retainBest and BFMatcher
+    cross check (mode 2)."""
     if kp_prev is None:
-        kp_prev = detect_and_compute(img_prev, nfeatures)
+        kp_prev = detect_and_compute(img_prev, nfeatures, semantics)
     kp1, d1 = kp_prev
-    kp2, d2 = detect_and_compute(img_cur, nfeatures)
-    q, t, d = bf_match(d1, d2, 1)
+    kp2, d2 = detect_and_compute(img_cur, nfeatures, semantics)
+    q, t, d = bf_match(d1, d2, 2 if semantics == OCV32 else 1)
     order = np.argsort(d, kind="stable")  # sorted(matches, key=distance), v3:221
     q, t = q[order], t[order]
     p1 = keypoints_to_points(kp1[q]).astype(np.float64)

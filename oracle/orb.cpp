@@ -22,6 +22,7 @@ const int kPattern[256 * 4] = {
 #include "../data/orb_bit_pattern_31.inc"
 };
 
+const int kOcv4 = 0, kOcv32 = 1;  // ora_*_v semantics: OpenCV 4.x (default) or 3.2
 const double kScaleFactor = (double)1.2f;  // ORB_Impl::scaleFactor (double member set from 1.2f)
 const int kEdgeThreshold = 31;
 const int kPatchSize = 31;
@@ -124,13 +125,92 @@ void resize_linear_exact(const Img& src, Img& dst, int dw, int dh) {
     }
 }
 
+// resize(INTER_LINEAR) as OpenCV 3.2 ran it for ORB's pyramid (imgwarp.cpp
+// resize -> resizeGeneric_ with HResizeLinear<uchar,int,short,2048> and
+// VResizeLinear<uchar,int,short,FixedPtCast<int,uchar,22>,VResizeLinearVec_32s8u>;
+// 4.x switched ORB to INTER_LINEAR_EXACT).  Per destination column:
+//   fx = (float)((dx + 0.5) * scale_x - 0.5), sx = cvFloor(fx), fx -= sx,
+//   clamped to sx = 0 / sx = W-1 (fx = 0) at the edges, and the 11-bit weights
+//   saturate_cast<short>((1 - fx) * 2048), saturate_cast<short>(fx * 2048)
+//   (each cvRound-ed on its own, so they may sum to 2047 or 2049);
+// rows the same with the source rows clipped to [0, H-1].  The horizontal
+// pass is exact int (S[sx] a0 + S[sx+1] a1; S[W-1] * 2048 past xmax).  The
+// vertical pass has two forms on x86: the SSE2 VResizeLinearVec_32s8u for
+// x < xs, ((mulhi(S0 >> 4, b0) + mulhi(S1 >> 4, b1) + 2) >> 2) in 16-bit
+// lanes, and the scalar FixedPtCast (S0 b0 + S1 b1 + 2^21) >> 22 for the last
+// columns; xs = where the 16-wide loop (x <= W-16) and then the 4-wide loop
+// (x < W-4) stop.  Assumes a build without IPP (distribution packages of 3.2
+// disable IPPICV).
+int ocv32_simd_end(int width) {
+    int x = 0;
+    for (; x <= width - 16; x += 16) {}
+    for (; x < width - 4; x += 4) {}
+    return x;
+}
+
+void resize_linear_32(const Img& src, Img& dst, int dw, int dh) {
+    dst.w = dw;
+    dst.h = dh;
+    dst.px.assign((size_t)dw * dh, 0);
+    const double scale_x = 1. / ((double)dw / src.w), scale_y = 1. / ((double)dh / src.h);
+    auto sat_short = [](float v) { return (int)std::max(-32768, std::min(32767, cv_round(v))); };
+    std::vector<int> xofs(dw), ia(2 * dw);
+    int xmax = dw;
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= src.w) {
+            xmax = std::min(xmax, dx);
+            if (sx >= src.w - 1) fx = 0, sx = src.w - 1;
+        }
+        xofs[dx] = sx;
+        ia[2 * dx] = sat_short((1.f - fx) * 2048);
+        ia[2 * dx + 1] = sat_short(fx * 2048);
+    }
+    auto hline = [&](int sy, std::vector<int>& out) {
+        const uint8_t* S = &src.px[(size_t)sy * src.w];
+        out.resize(dw);
+        for (int dx = 0; dx < dw; ++dx)
+            out[dx] = dx < xmax ? S[xofs[dx]] * ia[2 * dx] + S[xofs[dx] + 1] * ia[2 * dx + 1] : S[xofs[dx]] * 2048;
+    };
+    auto clip = [](int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; };
+    const int xs = ocv32_simd_end(dw);
+    std::vector<int> h0, h1;
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor(fy);
+        fy -= sy;
+        const int b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+        hline(clip(sy, 0, src.h), h0);
+        hline(clip(sy + 1, 0, src.h), h1);
+        uint8_t* d = &dst.px[(size_t)dy * dw];
+        for (int x = 0; x < dw; ++x) {
+            int v;
+            if (x < xs)  // _mm_mulhi_epi16 = (a * b) >> 16; the 16-bit adds never saturate here
+                v = ((((h0[x] >> 4) * b0) >> 16) + (((h1[x] >> 4) * b1) >> 16) + 2) >> 2;
+            else
+                v = (h0[x] * b0 + h1[x] * b1 + (1 << 21)) >> 22;
+            d[x] = (uint8_t)std::min(255, std::max(0, v));
+        }
+    }
+}
+
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on a pyramid ROI (orb.cpp
 // detectAndCompute).  ORB blurs a submatrix without BORDER_ISOLATED, so OpenCV
-// takes sepFilter2D's 8-bit fixed-point path: kernel = cvRound(256*g) =
-// {18,34,49,55,49,34,18}, int row sums, (sum + 2^15) >> 16 saturated.  The
-// reflect-101 border only feeds pixels the descriptor can never sample
-// (keypoints are >= 31 px from the level edge, patch reach <= 19), so clamping
-// vs. reflecting is immaterial; reflect-101 is used for fidelity anyway.
+// (3.2 and 4.x alike) takes sepFilter2D's 8-bit fixed-point path: kernel =
+// cvRound(256*g) = {18,34,49,55,49,34,18}, exact int row sums, and the column
+// pass SymmColumnFilter<FixedPtCastEx<int,uchar>, SymmColumnVec_32s8u>.  Its
+// vector op (SSE2 in 3.2, universal intrinsics in 4.x) covers every column up
+// to the last multiple of 4 in float with the kernel scaled by 2^-16: all
+// products and partial sums are exact there (< 2^24 units of 2^-16), so the
+// result is the exact sum, rounded half to even (cvtps2dq / v_round).  Only
+// the last w % 4 columns take the scalar FixedPtCastEx, (sum + 2^15) >> 16,
+// which rounds ties up.  The reflect-101 border only feeds pixels the
+// descriptor can never sample (keypoints are >= 31 px from the level edge,
+// patch reach <= 19), so clamping vs. reflecting is immaterial; reflect-101
+// is used for fidelity anyway.
 void gaussian_blur7(const Img& src, Img& dst) {
     // getGaussianKernel(7, 2, CV_32F), then convertTo(CV_32S, 256) (= cvRound).
     double sum = 0;
@@ -162,7 +242,8 @@ void gaussian_blur7(const Img& src, Img& dst) {
         for (int x = 0; x < w; ++x) {
             int s = 0;
             for (int i = 0; i < 7; ++i) s += k[i] * rows[(size_t)refl(y + i - 3, h) * w + x];
-            int v = (s + (1 << 15)) >> 16;
+            const int half_even = x < (w & ~3) ? (s >> 16) & 1 : 1;
+            int v = (s + (1 << 15) - 1 + half_even) >> 16;
             dst.px[(size_t)y * w + x] = (uint8_t)std::min(255, std::max(0, v));
         }
 }
@@ -299,14 +380,18 @@ void run_by_image_border(std::vector<KP>& kps, int w, int h, int border) {
 }
 
 // keypoint.cpp KeyPointsFilter::retainBest: nth_element + partition (libstdc++).
+// OpenCV 4.x selects the n-th best (nth_element at begin + n - 1); OpenCV 3.2
+// called nth_element at begin + n and then still read the boundary response
+// at index n - 1 (semantics == kOcv32), which keeps a different set whenever
+// responses tie at the boundary -- with FAST scores they usually do.
 template <class T, class Resp>
-void retain_best(std::vector<T>& kps, int n_points, Resp resp) {
+void retain_best(std::vector<T>& kps, int n_points, Resp resp, int semantics = kOcv4) {
     if (n_points >= 0 && kps.size() > (size_t)n_points) {
         if (n_points == 0) {
             kps.clear();
             return;
         }
-        std::nth_element(kps.begin(), kps.begin() + n_points - 1, kps.end(),
+        std::nth_element(kps.begin(), kps.begin() + n_points - (semantics == kOcv32 ? 0 : 1), kps.end(),
                          [&](const T& a, const T& b) { return resp(a) > resp(b); });
         float amb = resp(kps[n_points - 1]);
         auto new_end = std::partition(kps.begin() + n_points, kps.end(),
@@ -426,7 +511,7 @@ struct Pyramid {
     std::vector<float> scale;
 };
 
-Pyramid build_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels) {
+Pyramid build_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels, int semantics) {
     Pyramid P;
     P.lv.resize(nlevels);
     P.scale.resize(nlevels);
@@ -441,7 +526,10 @@ Pyramid build_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels)
             P.lv[0].px.resize((size_t)w * h);
             for (int y = 0; y < h; ++y) std::memcpy(&P.lv[0].px[(size_t)y * w], img + (size_t)y * stride, w);
         } else {
-            resize_linear_exact(P.lv[l - 1], P.lv[l], lw, lh);
+            if (semantics == kOcv32)
+                resize_linear_32(P.lv[l - 1], P.lv[l], lw, lh);
+            else
+                resize_linear_exact(P.lv[l - 1], P.lv[l], lw, lh);
         }
     }
     return P;
@@ -463,9 +551,9 @@ std::vector<int> features_per_level(int nfeatures, int nlevels) {
 
 // orb.cpp computeKeyPoints + detectAndCompute (no mask, useProvidedKeypoints=false)
 int detect_and_compute(const uint8_t* img, int w, int h, int stride, int nfeatures, std::vector<KP>& out,
-                       std::vector<uint8_t>& desc) {
+                       std::vector<uint8_t>& desc, int semantics) {
     const int nlevels = 8;
-    Pyramid P = build_pyramid(img, w, h, stride, nlevels);
+    Pyramid P = build_pyramid(img, w, h, stride, nlevels, semantics);
     std::vector<int> nper = features_per_level(nfeatures, nlevels);
     const int half = kPatchSize / 2;
     std::vector<int> umax = make_umax(half);
@@ -475,7 +563,7 @@ int detect_and_compute(const uint8_t* img, int w, int h, int stride, int nfeatur
         std::vector<KP> kps;
         fast16(P.lv[l].px.data(), P.lv[l].w, P.lv[l].h, P.lv[l].w, kFastThreshold, kps);
         run_by_image_border(kps, P.lv[l].w, P.lv[l].h, kEdgeThreshold);
-        retain_best(kps, 2 * nper[l], [](const KP& k) { return k.response; });
+        retain_best(kps, 2 * nper[l], [](const KP& k) { return k.response; }, semantics);
         counters[l] = (int)kps.size();
         float sf = P.scale[l];
         for (auto& k : kps) {
@@ -501,7 +589,7 @@ int detect_and_compute(const uint8_t* img, int w, int h, int stride, int nfeatur
     for (int l = 0; l < nlevels; ++l) {
         std::vector<KP> kps(all.begin() + off, all.begin() + off + counters[l]);
         off += counters[l];
-        retain_best(kps, nper[l], [](const KP& k) { return k.response; });
+        retain_best(kps, nper[l], [](const KP& k) { return k.response; }, semantics);
         newall.insert(newall.end(), kps.begin(), kps.end());
     }
     all.swap(newall);
@@ -659,7 +747,12 @@ int ora_orb_features_per_level(int nfeatures, int nlevels, int* out) {
 }
 
 int ora_orb_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels, int blurred, uint8_t* out) {
-    Pyramid P = build_pyramid(img, w, h, stride, nlevels);
+    return ora_orb_pyramid_v(img, w, h, stride, nlevels, blurred, kOcv4, out);
+}
+
+int ora_orb_pyramid_v(const uint8_t* img, int w, int h, int stride, int nlevels, int blurred, int semantics,
+                      uint8_t* out) {
+    Pyramid P = build_pyramid(img, w, h, stride, nlevels, semantics);
     size_t off = 0;
     for (int l = 0; l < nlevels; ++l) {
         Img b;
@@ -688,15 +781,23 @@ int ora_fast(const uint8_t* img, int w, int h, int stride, int threshold, int32_
 }
 
 int ora_retain_best(const float* resp, int n, int n_points, int32_t* perm) {
+    return ora_retain_best_v(resp, n, n_points, kOcv4, perm);
+}
+
+int ora_retain_best_v(const float* resp, int n, int n_points, int semantics, int32_t* perm) {
     struct E { float r; int32_t i; };
     std::vector<E> v(n);
     for (int i = 0; i < n; ++i) v[i] = E{resp[i], i};
-    retain_best(v, n_points, [](const E& e) { return e.r; });
+    retain_best(v, n_points, [](const E& e) { return e.r; }, semantics);
     for (size_t i = 0; i < v.size(); ++i) perm[i] = v[i].i;
     return (int)v.size();
 }
 
 int ora_retain_best_depth(const float* resp, int n, int n_points, int depth, int32_t* perm) {
+    return ora_retain_best_depth_v(resp, n, n_points, depth, kOcv4, perm);
+}
+
+int ora_retain_best_depth_v(const float* resp, int n, int n_points, int depth, int semantics, int32_t* perm) {
     std::vector<float> v(resp, resp + n);
     std::vector<int32_t> p(n);
     for (int i = 0; i < n; ++i) p[i] = i;
@@ -711,7 +812,7 @@ int ora_retain_best_depth(const float* resp, int n, int n_points, int depth, int
         while ((2 << lg) <= n) ++lg;  // std::__lg(n)
         depth = 2 * lg;
     }
-    s.introselect(0, n_points - 1, n, depth);
+    s.introselect(0, n_points - (semantics == kOcv32 ? 0 : 1), n, depth);
     float amb = v[n_points - 1];
     // std::partition (bidirectional) on [n_points, n) with pred resp >= amb
     int first = n_points, last = n;
@@ -737,9 +838,15 @@ done:
 
 int ora_orb_detect_and_compute(const uint8_t* img, int w, int h, int stride, int nfeatures, ora_keypoint* kps,
                                uint8_t* desc, int cap, int* n_out) {
+    return ora_orb_detect_and_compute_v(img, w, h, stride, nfeatures, kOcv4, kps, desc, cap, n_out);
+}
+
+int ora_orb_detect_and_compute_v(const uint8_t* img, int w, int h, int stride, int nfeatures, int semantics,
+                                 ora_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+    if (semantics != kOcv4 && semantics != kOcv32) return -2;
     std::vector<KP> out;
     std::vector<uint8_t> d;
-    detect_and_compute(img, w, h, stride, nfeatures, out, d);
+    detect_and_compute(img, w, h, stride, nfeatures, out, d, semantics);
     *n_out = (int)out.size();
     if ((int)out.size() > cap) return -1;
     for (size_t i = 0; i < out.size(); ++i) {

@@ -1,0 +1,123 @@
+"""OpenCV 3.2 semantics on the GPU (include/dvo.h DVO_OPENCV_32), bit-exact
+against the oracle in the same mode (oracle/orb.cpp resize_linear_32 and
+retain_best's 3.2 branch; oracle.py pair_pose(semantics=OCV32)).
+
+The reference pins no OpenCV version; its Python 2.7 .pyc files and ROS
+Melodic docs make 3.2 the likely one, while the default path
+follows 4.x.  Parity against OpenCV itself stays unpinned in both modes: no
+cv2 build exists in this container or on the GPU box."""
+import numpy as np
+import pytest
+
+from conftest import synth_frames
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,npoints", [(10, 3), (1000, 217), (5000, 434), (20000, 868), (333, 332)])
+def test_retain_best_opencv32(gpu_ctx, oracle_mod, n, npoints):
+    from droplet_visual_odometry_amd import ops
+    rng = np.random.default_rng(n)
+    for r in (rng.integers(21, 60, n).astype(np.float32), rng.standard_normal(n).astype(np.float32),
+              np.full(n, 5.0, np.float32)):
+        want = oracle_mod.retain_best(r, npoints, semantics=oracle_mod.OCV32)
+        got = ops.test_retain_best(r, npoints, opencv="3.2", ctx=gpu_ctx)
+        np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("depth", [0, 2])
+def test_retain_best_opencv32_heap_select(gpu_ctx, oracle_mod, depth):
+    from droplet_visual_odometry_amd import ops
+    r = np.random.default_rng(depth).integers(0, 40, 3000).astype(np.float32)
+    np.testing.assert_array_equal(ops.test_retain_best(r, 300, depth=depth, opencv="3.2", ctx=gpu_ctx),
+                                  oracle_mod.retain_best(r, 300, depth=depth, semantics=oracle_mod.OCV32))
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (1280, 720), (1067, 601), (37, 29)])
+def test_pyramid_opencv32(gpu_ctx, oracle_mod, W, H):
+    """Every INTER_LINEAR level and every blurred level; widths that leave 1-3
+    scalar-tail columns (1067 -> 889 ...) and a tiny frame."""
+    import torch
+    from droplet_visual_odometry_amd.stream import FrameStream
+    if (W, H) in ((640, 480), (1280, 720)):
+        frames, K = synth_frames(W, H, [0, 1])
+    else:
+        rng = np.random.default_rng(W)
+        frames = rng.integers(0, 256, (2, H, W)).astype(np.uint8)
+        K = np.array([[W, 0, W / 2], [0, W, H / 2], [0, 0, 1.0]])
+    fs = FrameStream(W, H, K, nfeatures=500, max_frames=2, ctx=gpu_ctx, opencv="3.2")
+    fs.process(torch.from_numpy(np.ascontiguousarray(frames)).cuda())
+    fs.sync()
+    want = oracle_mod.pyramid(frames[1], semantics=oracle_mod.OCV32)
+    want_b = oracle_mod.pyramid(frames[1], blurred=True, semantics=oracle_mod.OCV32)
+    for l in range(8):
+        if l:
+            np.testing.assert_array_equal(fs.pyramid(1, l), want[l], err_msg=f"level {l}")
+        np.testing.assert_array_equal(fs.pyramid(1, l, blurred=True), want_b[l], err_msg=f"blurred level {l}")
+    fs.close()
+
+
+@pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])
+def test_detect_and_compute_opencv32(gpu_ctx, oracle_mod, W, H, NF):
+    from droplet_visual_odometry_amd import ops
+    frames, _ = synth_frames(W, H, [0, 1])
+    for f in frames:
+        kg, dg = ops.detect_and_compute(f, NF, opencv="3.2", ctx=gpu_ctx)
+        ko, do = oracle_mod.detect_and_compute(f, NF, semantics=oracle_mod.OCV32)
+        assert len(kg) == len(ko) == NF
+        np.testing.assert_array_equal(kg.view(np.uint8), ko.view(np.uint8))
+        np.testing.assert_array_equal(dg, do)
+        k4, _ = oracle_mod.detect_and_compute(f, NF)
+        assert not np.array_equal(k4.view(np.uint8), ko.view(np.uint8))  # the modes really differ
+
+
+@pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])
+def test_stream_pairs_opencv32(gpu_ctx, oracle_mod, W, H, NF):
+    """The whole per-pair path in 3.2 mode (ORB 3.2, 3.x cross check):
+    keypoints, matches, E, R, t, RANSAC iterations bit-exact vs the oracle."""
+    import torch
+    from droplet_visual_odometry_amd.stream import FrameStream
+    frames, K = synth_frames(W, H, range(4))
+    fs = FrameStream(W, H, K, nfeatures=NF, max_frames=4, ctx=gpu_ctx, opencv="3.2")
+    rec = fs.process(torch.from_numpy(np.ascontiguousarray(frames)).cuda())
+    fs.sync()
+    recs = FrameStream.records_numpy(rec, 3)
+    kp_prev = None
+    for i in range(3):
+        ref = oracle_mod.pair_pose(frames[i], frames[i + 1], K, NF, kp_prev=kp_prev, semantics=oracle_mod.OCV32)
+        kp_prev = (ref["kp_cur"], ref["desc_cur"])
+        kg, dg = fs.features(i + 1)
+        np.testing.assert_array_equal(kg.view(np.uint8), ref["kp_cur"].view(np.uint8))
+        np.testing.assert_array_equal(dg, ref["desc_cur"])
+        mg = fs.matches(i)
+        np.testing.assert_array_equal(mg["queryIdx"], ref["q"])
+        np.testing.assert_array_equal(mg["trainIdx"], ref["t"])
+        r = recs[i]
+        assert r["status"] == 0 and r["ransac_iters"] == ref["iters"]
+        np.testing.assert_array_equal(r["E"].reshape(3, 3), ref["E"])
+        np.testing.assert_array_equal(r["R"].reshape(3, 3), ref["R"])
+        np.testing.assert_array_equal(r["t"], ref["t_unit"].ravel())
+    fs.close()
+
+
+def test_dropin_cv_semantics_switch(gpu_ctx, oracle_mod):
+    """cv.OPENCV_SEMANTICS = "3.2" makes the cv2 stand-ins (ORB_create,
+    BFMatcher crossCheck) the 3.2 ones."""
+    from droplet_visual_odometry_amd import cv
+    frames, _ = synth_frames(640, 480, [0, 1])
+    old = cv.OPENCV_SEMANTICS
+    try:
+        cv.OPENCV_SEMANTICS = "3.2"
+        orb = cv.ORB_create()
+        bf = cv.BFMatcher(cv.NORM_HAMMING, crossCheck=True)
+        assert bf.legacy_crosscheck
+        k0, d0 = orb.detectAndCompute(frames[0], None)
+        k1, d1 = orb.detectAndCompute(frames[1], None)
+        ko0, do0 = oracle_mod.detect_and_compute(frames[0], 500, semantics=oracle_mod.OCV32)
+        ko1, do1 = oracle_mod.detect_and_compute(frames[1], 500, semantics=oracle_mod.OCV32)
+        np.testing.assert_array_equal(d0, do0)
+        m = bf.match(d0, d1)
+        q, t, _ = oracle_mod.bf_match(do0, do1, 2)
+        assert [x.queryIdx for x in m] == list(q) and [x.trainIdx for x in m] == list(t)
+    finally:
+        cv.OPENCV_SEMANTICS = old

@@ -1,12 +1,13 @@
 """One stream sharded across ranks on the GPU (BASELINE configs[3], SURVEY.md
-§8e): each rank runs FrameStream.process + pose_tail on its run of pairs with
-the left halo frame, the ranks exchange records and T_rel
-(dist.ShardedPoseStream; gloo through host memory here, since the two ranks
-share the box's one GPU — RCCL in bench.py on a multi-GPU node), and rank 0
-chains T_abs on the device (stream.PoseChain).  The result must equal one rank
-processing the whole stream: records, T_rel and T_abs bit for bit
-(trajectory_evaluation_dual_process.py:172-252 is the single-stream loop;
-visual_odometry_v3.py:264, :344, :367 couple adjacent pairs)."""
+§8e): each rank runs FrameStream.process on its run of pairs, the ranks
+all-gather records and marker corners (dist.ShardedPoseStream; gloo through
+host memory here, since two ranks share the box's one GPU; RCCL at world size
+1 below, and across GPUs in bench.py on a multi-GPU node), and rank 0 runs the
+window's pose tail from the gathered records (stream.PoseTail).  The result
+must equal one rank processing the whole stream: records, T_rel and T_abs bit
+for bit (trajectory_evaluation_dual_process.py:172-252 is the single-stream
+loop; visual_odometry_v3.py:264, :344, :367 couple adjacent pairs) -- also
+when featureless frames make the pairs at a shard boundary fail."""
 import os
 import socket
 
@@ -15,8 +16,6 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-W, H, NF = 640, 480, 500
-
 
 def _free_port():
     with socket.socket() as s:
@@ -24,7 +23,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n_pairs, windows, out):
+def _stream(W, H, F, blank):
+    """F synthetic frames + marker corners; frames in `blank` are featureless
+    and keep the previous frame's corners."""
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd.synth import marker_corners
+    frames, K = synth_frames(W, H, range(F))
+    frames = frames.copy()
+    corners = [marker_corners(i, K) for i in range(F)]
+    for b in blank:
+        frames[b] = 90
+        corners[b] = corners[b - 1]
+    return frames, np.stack(corners), K
+
+
+def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, streams, out):
     import faulthandler
     import sys
     import torch
@@ -34,74 +47,105 @@ def _worker(rank, world, port, n_pairs, windows, out):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
     sys.path.insert(0, os.path.dirname(here))
-    from conftest import synth_frames
     from droplet_visual_odometry_amd import dist as ddist
     from droplet_visual_odometry_amd._native import Context
-    from droplet_visual_odometry_amd.stream import FrameStream, PoseChain
-    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    F = n_pairs * windows + 1
-    frames, K = synth_frames(W, H, range(F))
     dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames, corners, K = _stream(W, H, n_pairs * windows + 1, blank)
     d_frames = torch.from_numpy(frames).to(dev)
-    d_corners = torch.from_numpy(np.stack([marker_corners(i, K) for i in range(F)])).to(dev)
-    ctx = Context(0)
-    sh = ddist.ShardedPoseStream(world, rank, n_pairs, dev, host_gather=True)
-    fs = FrameStream(W, H, K, nfeatures=NF, max_frames=sh.cap + 2, ctx=ctx)
-    fs.reset_pose()
-    recs = fs.new_records(sh.cap + 1)
-    T_rel = torch.zeros((sh.cap + 1, 4, 4), dtype=torch.float64, device=dev)
-    T_abs = torch.zeros((sh.cap + 1, 4, 4), dtype=torch.float64, device=dev)
-    chain = PoseChain(ctx)
+    d_corners = torch.from_numpy(corners).to(dev)
+    run = ddist.ShardedStreamRunner(W, H, K, NF, n_pairs, world, rank, MARKER_LEN, ctx=Context(0),
+                                    streams=streams, host_gather=backend == "gloo")
     got_rec, got_Trel, got_Tabs = [], [], []
+    pending = []
     for w in range(windows):
-        p0, p1, f0, f1, halo = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
-        fs.process(d_frames[f0:f1], recs)
-        fs.pose_tail(d_corners[f0:f1 - 1], d_corners[f0 + 1:f1], MARKER_LEN, T_rel, T_abs)
-        fs.sync()
-        all_rec, all_T = sh.exchange(recs, T_rel, halo)
-        got_rec.append(all_rec.numpy().copy())
-        got_Trel.append(all_T.numpy().copy())
-        if rank == 0:
-            got_Tabs.append(chain.run(all_T.to(dev).contiguous()).cpu().numpy())
-    torch.cuda.synchronize()
-    out[rank] = (np.concatenate(got_rec).tobytes(), np.concatenate(got_Trel).tobytes(),
+        p0, p1, f0, f1 = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
+        recs, T_rel, T_abs = run.step(d_frames[f0:f1], d_corners[f0:f1 - 1], d_corners[f0 + 1:f1])
+        # device copies on torch's stream (ordered after the collective / the tail), read back
+        # only at the end: no host sync between windows, so slots are reused while in flight
+        pending.append((recs.clone(), T_rel.clone() if T_rel is not None else None,
+                        T_abs.clone() if T_abs is not None else None))
+    run.sync()
+    for recs, T_rel, T_abs in pending:
+        got_rec.append(recs.cpu().numpy())
+        if T_rel is not None:
+            got_Trel.append(T_rel.cpu().numpy())
+            got_Tabs.append(T_abs.cpu().numpy())
+    out[rank] = (np.concatenate(got_rec).tobytes(),
+                 np.concatenate(got_Trel).tobytes() if got_Trel else b"",
                  np.concatenate(got_Tabs).tobytes() if got_Tabs else b"")
-    fs.close()
+    run.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_pairs,windows", [(6, 2), (5, 1)])
-def test_sharded_stream_equals_single_rank(gpu_ctx, n_pairs, windows):
+def _single_rank(ctx, W, H, NF, F, blank):
     import torch
-    import torch.multiprocessing as mp
-    from conftest import synth_frames
     from droplet_visual_odometry_amd.stream import FrameStream
-    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
-    F = n_pairs * windows + 1
-    frames, K = synth_frames(W, H, range(F))
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_worker, args=(2, _free_port(), n_pairs, windows, out), nprocs=2, join=True)
-    fs = FrameStream(W, H, K, nfeatures=NF, max_frames=F, ctx=gpu_ctx)
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    frames, corners, K = _stream(W, H, F, blank)
+    fs = FrameStream(W, H, K, nfeatures=NF, max_frames=F, ctx=ctx)
     fs.reset_pose()
     rec = fs.process(torch.from_numpy(frames).cuda())
-    dc = torch.from_numpy(np.stack([marker_corners(i, K) for i in range(F)])).cuda()
+    dc = torch.from_numpy(corners).cuda()
     T_rel, T_abs = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
     fs.sync()
-    want_rec = rec.cpu().numpy().tobytes()
-    want_Trel = T_rel.cpu().numpy()
-    want_Tabs = T_abs.cpu().numpy()
+    out = rec.cpu().numpy().tobytes(), T_rel.cpu().numpy(), T_abs.cpu().numpy()
     fs.close()
-    for r in range(2):
-        got_rec, got_Trel, got_Tabs = out[r]
-        assert got_rec == want_rec, f"rank {r}: gathered records differ from the single-rank stream"
-        np.testing.assert_array_equal(np.frombuffer(got_Trel).reshape(-1, 4, 4), want_Trel)
+    return out
+
+
+def _check(gpu_ctx, out, ranks, W, H, NF, F, blank):
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+    want_rec, want_Trel, want_Tabs = _single_rank(gpu_ctx, W, H, NF, F, blank)
+    st = np.frombuffer(want_rec, PAIR_RECORD_DTYPE)["status"]
+    for b in blank:  # the blank frame's two pairs fail in the single-rank run too
+        assert st[b - 1] != 0 and st[b] != 0
+    for r in range(ranks):
+        assert out[r][0] == want_rec, f"rank {r}: gathered records differ from the single-rank stream"
+    np.testing.assert_array_equal(np.frombuffer(out[0][1]).reshape(-1, 4, 4), want_Trel)
     got_Tabs = np.frombuffer(out[0][2]).reshape(-1, 4, 4)
     bad = [i for i in range(len(want_Tabs)) if not np.array_equal(got_Tabs[i], want_Tabs[i])]
-    assert not bad, f"rank 0 chained T_abs differs at pairs {bad}"
+    assert not bad, f"rank 0 T_abs differs at pairs {bad}"
+
+
+@pytest.mark.parametrize("W,H,NF,n_pairs,windows,blank", [
+    (640, 480, 500, 6, 2, ()),
+    (640, 480, 500, 5, 1, ()),
+    # BASELINE configs[3] workload; frame 3 is rank 1's first frame, so pairs 2 (rank 0) and 3
+    # (rank 1) fail and pair 4 triangulates against pair 1's P (rank 0); frame 6 fails the last
+    # pair of window 0 and the first of window 1, so pair 7 uses pair 4's P from the carry
+    (1280, 720, 2000, 6, 2, (3, 6)),
+])
+def test_sharded_stream_equals_single_rank(gpu_ctx, W, H, NF, n_pairs, windows, blank):
+    import torch.multiprocessing as mp
+    F = n_pairs * windows + 1
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), "gloo", W, H, NF, n_pairs, windows, blank, 1, out), nprocs=2, join=True)
+    _check(gpu_ctx, out, 2, W, H, NF, F, blank)
+
+
+def test_sharded_rccl_path_two_slots_in_flight(gpu_ctx):
+    """The RCCL branch of the sharded loop (device all-gather, no host syncs):
+    world size 1 on the box's one GPU, two send-buffer slots in flight over six
+    windows, so every slot is rewritten while the previous windows' collectives
+    and pose tails are still queued.  Any missing stream order (records read
+    before written, a send buffer rewritten before its collective read it, the
+    tail racing the gather) shows as a mismatch with the single-rank stream."""
+    import torch.multiprocessing as mp
+    W, H, NF, n_pairs, windows, blank = 640, 480, 500, 8, 6, (12,)
+    F = n_pairs * windows + 1
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(1, _free_port(), "nccl", W, H, NF, n_pairs, windows, blank, 2, out), nprocs=1, join=True)
+    _check(gpu_ctx, out, 1, W, H, NF, F, blank)
 
 
 def test_pose_chain_equals_pose_tail_chain(gpu_ctx):

@@ -124,6 +124,74 @@ def test_retain_best_restated_introselect_matches_libstdcxx(oracle_mod):
             assert set(kept.tolist()) == set(np.nonzero(r >= kth)[0].tolist())
 
 
+def test_retain_best_opencv32_semantics(oracle_mod):
+    """OpenCV 3.2's retainBest (nth_element at n, boundary read at n - 1): the
+    restated introselect equals libstdc++'s std::nth_element in this mode too;
+    the kept set holds the n best, plus the tail entries tying the response now
+    at index n - 1; and it differs from 4.x's when responses tie at the
+    boundary (FAST scores are integers, so they usually do)."""
+    rng = np.random.default_rng(1)
+    differs = 0
+    for n, k in [(4, 1), (5, 2), (17, 5), (100, 50), (1000, 217), (4000, 3999)]:
+        for r in (rng.integers(0, 9, n).astype(np.float32), rng.standard_normal(n).astype(np.float32)):
+            kept = oracle_mod.retain_best(r, k, semantics=oracle_mod.OCV32)
+            np.testing.assert_array_equal(oracle_mod.retain_best(r, k, depth=-1, semantics=oracle_mod.OCV32), kept)
+            assert len(kept) >= k
+            kth = np.sort(r)[::-1][k - 1]
+            assert set(np.nonzero(r > kth)[0].tolist()) <= set(kept.tolist()) <= set(np.nonzero(r >= kth)[0].tolist())
+            differs += set(kept.tolist()) != set(oracle_mod.retain_best(r, k).tolist())
+    assert differs > 0
+
+
+def test_opencv32_pyramid_kats(oracle_mod):
+    """resize(INTER_LINEAR) as 3.2 ran it: a constant image stays constant
+    wherever both 11-bit weights round to a 2048 sum, the SSE2 / scalar split
+    sits where its loops stop, and the 3.2 pyramid differs from 4.x's
+    INTER_LINEAR_EXACT one on a textured frame (level 0 is the input in both)."""
+    from conftest import synth_frames
+    frames, _ = synth_frames(640, 480, [0])
+    a = oracle_mod.pyramid(frames[0], semantics=oracle_mod.OCV4)
+    b = oracle_mod.pyramid(frames[0], semantics=oracle_mod.OCV32)
+    np.testing.assert_array_equal(a[0], b[0])
+    assert all(x.shape == y.shape for x, y in zip(a, b))
+    assert any(not np.array_equal(x, y) for x, y in zip(a[1:], b[1:]))
+    # the SSE2 vertical pass truncates twice (h >> 4, mulhi): each 3.2 level comes out about
+    # 0.12 grey levels darker than the bit-exact one, and levels are resized from levels
+    for l in range(1, 8):
+        d = b[l].astype(int) - a[l].astype(int)
+        assert -0.15 * l < float(d.mean()) < -0.09 * l and np.abs(d).max() <= 3
+    for v in (0, 1, 128, 255):
+        lv = oracle_mod.pyramid(np.full((96, 128), v, np.uint8), semantics=oracle_mod.OCV32)
+        for L in lv:
+            assert abs(int(L.min()) - v) <= 1 and abs(int(L.max()) - v) <= 1
+
+
+def test_blur_rounds_ties_half_even_except_last_columns(oracle_mod):
+    """GaussianBlur's column pass (SymmColumnVec_32s8u) rounds sum / 2^16 half to
+    even in float; only the last w % 4 columns take the scalar (sum + 2^15) >> 16.
+    Checked against exact integer sums on a frame with ties."""
+    from conftest import synth_frames
+    frames, _ = synth_frames(640, 480, [1])
+    k = np.array([18, 34, 49, 55, 49, 34, 18])
+
+    def refl(n):
+        i = np.arange(-3, n + 3)
+        i = np.where(i < 0, -i, i)
+        return np.where(i >= n, 2 * n - 2 - i, i)
+    ties = 0
+    for L, B in zip(oracle_mod.pyramid(frames[0]), oracle_mod.pyramid(frames[0], blurred=True)):
+        h, w = L.shape
+        a = L.astype(np.int64)[:, refl(w)]
+        rows = sum(k[i] * a[:, i:i + w] for i in range(7))[refl(h), :]
+        S = sum(k[i] * rows[i:i + h, :] for i in range(7))
+        want = np.minimum((S + 32768) >> 16, 255)
+        he = np.minimum((S + 32767 + ((S >> 16) & 1)) >> 16, 255)
+        want[:, :w & ~3] = he[:, :w & ~3]
+        np.testing.assert_array_equal(B, want)
+        ties += int(((S & 0xFFFF) == 0x8000).sum())
+    assert ties > 0
+
+
 def test_bf_match_tie_rules(oracle_mod):
     d = np.zeros((4, 32), np.uint8)
     d[1, 0] = 1      # distance 1 from d[0]
