@@ -984,7 +984,9 @@ int sift_plan(dvo_ctx* ctx, int w, int h) {
     sig[0] = sig0;
     const double k = std::pow(2., 1. / 3);
     for (int i = 1; i < 6; ++i) {
-        const double sig_prev = std::pow(k, (double)(i - 1)) * 1.6f, sig_total = sig_prev * k;
+        // buildGaussianPyramid uses SIFT_Impl's double member sigma (1.6, not 1.6f);
+        // only createInitialImage and adjustLocalExtrema take it as float
+        const double sig_prev = std::pow(k, (double)(i - 1)) * 1.6, sig_total = sig_prev * k;
         sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
     }
     for (int i = 0; i < 6; ++i) {

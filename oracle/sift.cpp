@@ -30,7 +30,8 @@ namespace {
 constexpr int kLayers = 3;                // nOctaveLayers
 constexpr float kContrast = 0.04f;        // contrastThreshold
 constexpr float kEdge = 10.f;             // edgeThreshold
-constexpr float kSigma = 1.6f;            // sigma
+constexpr float kSigma = 1.6f;            // sigma as createInitialImage / adjustLocalExtrema see it (float)
+constexpr double kSigmaD = 1.6;           // SIFT_Impl::sigma (double member), used by buildGaussianPyramid
 constexpr int kFirstOctave = -1;          // the input is upscaled 2x
 constexpr int kBorder = 5;                // SIFT_IMG_BORDER
 constexpr int kMaxInterp = 5;             // SIFT_MAX_INTERP_STEPS
@@ -375,10 +376,12 @@ int ora_sift_detect_and_compute(const uint8_t* img, int w, int h, int stride, or
     const int nOct = cv_round_d(std::log((double)std::min(base.w, base.h)) / std::log(2.) - 2) - kFirstOctave;
     // buildGaussianPyramid
     std::vector<double> sig(kLayers + 3);
-    sig[0] = kSigma;
+    sig[0] = kSigmaD;
     const double k = std::pow(2., 1. / kLayers);
     for (int i = 1; i < kLayers + 3; i++) {
-        const double sig_prev = std::pow(k, (double)(i - 1)) * kSigma, sig_total = sig_prev * k;
+        // SIFT_Impl::buildGaussianPyramid: the double member sigma = 1.6 (createInitialImage and
+        // adjustLocalExtrema take it as float, hence kSigma elsewhere)
+        const double sig_prev = std::pow(k, (double)(i - 1)) * kSigmaD, sig_total = sig_prev * k;
         sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
     }
     std::vector<FImg> gp((size_t)nOct * (kLayers + 3));

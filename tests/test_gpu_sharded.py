@@ -16,6 +16,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+W, H, NF = 640, 480, 500  # the single-rank pose-tail tests below
+
 
 def _free_port():
     with socket.socket() as s:

@@ -82,3 +82,59 @@ def test_gt_vo_difference_files(tmp_path):
     out = tmp_path / "diff.txt"
     pem.write_gt_vo_difference_to_file(str(gt), str(vo), str(out))
     assert out.read_text().startswith("at timestamp 1.0 the gt vo euler angle difference is ")
+
+
+def _tf_log():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tf_log_transforms.json")
+    return json.load(open(path))["transforms"]
+
+
+def test_real_tf_log_round_trips_through_the_pose_helpers():
+    """The 454 ROS tf transforms the reference's author logged
+    (scripts/back_up_files/log.txt, transcribed by
+    tests/golden/make_tf_log_kats.py): STag marker poses in the camera frame,
+    base_link and the AHRS orientation.  For each one,
+    transformation_from_translation_quaternion (pem:15-23, tf.quaternion_matrix)
+    followed by quaternion_from_transformation_matrix (pem:60-65 -> the trace
+    branches of pem:31-57) returns the logged (x, y, z, w) up to sign, and
+    translation_from_transformation_matrix (pem:26-28) the logged translation
+    exactly.  Every trace branch the real data reaches is exercised."""
+    logs = _tf_log()
+    assert len(logs) == 454
+    branches = set()
+    for e in logs:
+        t, q = e["t"], np.array(e["q"])
+        assert abs(np.linalg.norm(q) - 1) < 1e-9, e["line"]  # ROS publishes unit quaternions (to print precision)
+        T = pem.transformation_from_translation_quaternion(t, q)
+        np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-9)
+        assert pem.translation_from_transformation_matrix(T) == t
+        got = np.array(pem.quaternion_from_transformation_matrix(T))
+        assert _same_rotation_tol(got, q, 1e-9), (e["line"], got, q)
+        R = T[:3, :3]
+        tr_ = np.trace(R)
+        branches.add("trace" if tr_ > 0 else ("r00" if R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]
+                                               else ("r11" if R[1, 1] > R[2, 2] else "r22")))
+    assert {"trace", "r00"} <= branches, branches
+
+
+def _same_rotation_tol(q1, q2, tol):
+    return np.allclose(q1, q2, atol=tol) or np.allclose(q1, -q2, atol=tol)
+
+
+def test_real_tf_log_marker_to_marker_motion_is_rigid():
+    """Consecutive logged poses of one marker composed the way the harness does
+    (get_marker_to_marker_transformation, pem: marker pose at t-1 inverted times
+    the pose at t) give proper rigid motions whose quaternion round-trips too."""
+    logs = [e for e in _tf_log() if e["child_frame_id"] == "/ar_marker_0"]
+    Ts = [pem.transformation_from_translation_quaternion(e["t"], e["q"]) for e in logs]
+    for a, b in zip(Ts, Ts[1:]):
+        M = pem.get_marker_to_marker_transformation(a, b)
+        R = M[:3, :3]
+        np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-9)
+        assert abs(np.linalg.det(R) - 1) < 1e-9
+        q = pem.quaternion_from_transformation_matrix(M)
+        M2 = pem.transformation_from_translation_quaternion(pem.translation_from_transformation_matrix(M),
+                                                            np.array(q) / np.linalg.norm(q))
+        np.testing.assert_allclose(M2, M, atol=1e-9)
