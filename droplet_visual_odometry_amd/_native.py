@@ -101,6 +101,7 @@ _SIGNATURES = {
     "dvo_orb_detect_and_compute": ([_vp, ctypes.POINTER(OrbParams), _vp, _c, _c, _c, _vp, _vp, _c, _ip], _c),
     "dvo_bf_match_hamming": ([_vp, _vp, _c, _vp, _c, _c, _vp, _c, _ip], _c),
     "dvo_bf_knn_float": ([_vp, _vp, _c, _vp, _c, _c, _c, _c, _vp, _vp], _c),
+    "dvo_flann_knn": ([_vp, _vp, _c, _vp, _c, _c, _c, _c, _c, ctypes.POINTER(ctypes.c_uint64), _vp, _vp], _c),
     "dvo_sift_detect_and_compute": ([_vp, _vp, _c, _c, _c, _vp, _vp, _c, _ip], _c),
     "dvo_surf_detect_and_compute": ([_vp, _vp, _c, _c, _c, ctypes.c_double, _vp, _vp, _c, _ip], _c),
     "dvo_find_essential_mat": ([_vp, _vp, _vp, _c, _vp, _d, _d, _c, _vp, _ip, _vp], _c),

@@ -937,6 +937,129 @@ int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int
 }
 
 namespace {
+// cv::theRNG()'s multiply-with-carry s' = (u32)s * A + (s >> 32) is s' = s * A mod m,
+// m = A * 2^32 - 1, for every state below m (all but a few seeds): jump k steps ahead.
+constexpr uint64_t kTheRngA = 4164903690ull;
+uint64_t therng_jump(uint64_t s, uint64_t k) {
+    const unsigned __int128 m = ((unsigned __int128)kTheRngA << 32) - 1;
+    if (k > 0 && (unsigned __int128)s >= m) {  // a seed at or above m: one plain step lands below m
+        s = (uint64_t)(uint32_t)s * kTheRngA + (s >> 32);
+        --k;
+    }
+    unsigned __int128 r = s, b = kTheRngA;
+    for (; k; k >>= 1) {
+        if (k & 1) r = r * b % m;
+        b = b * b % m;
+    }
+    return (uint64_t)r;
+}
+}  // namespace
+
+// Replaces cv::FlannBasedMatcher(KDTREE, trees).knnMatch(query, train, k) with
+// search checks (the 'flann' mode, visual_odometry_v3.py:206-212); flann.hip.
+int dvo_flann_knn(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int trees,
+                  int checks, uint64_t* rng_state, int32_t* train_idx, float* dist) {
+    if (!ctx) return DVO_EINVAL;
+    if (!rng_state) return fail(ctx, DVO_EINVAL, "null theRNG state");
+    if (dim < 4 || dim > 256 || dim % 4) return fail(ctx, DVO_EINVAL, "dim must be a multiple of 4 in 4..256");
+    if (k < 1 || k > 4) return fail(ctx, DVO_EINVAL, "k must be 1..4");
+    if (trees < 1 || trees > 64 || checks < 1) return fail(ctx, DVO_EINVAL, "trees 1..64 and checks >= 1");
+    if (nq < 0 || nt < 0 || nq > (1 << 20) || nt > (1 << 16))
+        return fail(ctx, DVO_EINVAL, "descriptor counts out of range (queries 0..2^20, train 0..2^16)");
+    // DescriptorMatcher::knnMatch returns before training on an empty query or train set
+    if (nq == 0 || nt == 0) return DVO_OK;
+    if (!dq || !dt || !train_idx || !dist) return fail(ctx, DVO_EINVAL, "null buffer");
+    if (k > nt) return fail(ctx, DVO_EINVAL, "k exceeds the train set (FLANN asserts knn <= index size)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int n = nt, draws = 2 * n - 1, nodes_per_tree = 2 * n - 1;
+    constexpr int kChunks = 64;
+    void *bq, *bt, *bR, *bcs, *bcnt, *boff, *bfill, *blist, *bind, *bind2, *bxv, *bsl, *bsr, *bnodes, *bopen, *blev,
+        *bidx, *bdist, *bflag, *bredo;
+    int rc;
+    if ((rc = scratch(ctx, 40, (size_t)nq * dim * 4, &bq)) || (rc = scratch(ctx, 41, (size_t)nt * dim * 4, &bt)) ||
+        (rc = scratch(ctx, 42, (size_t)draws * 4, &bR)) || (rc = scratch(ctx, 43, (size_t)trees * kChunks * 8, &bcs)) ||
+        (rc = scratch(ctx, 44, (size_t)n * 4, &bcnt)) || (rc = scratch(ctx, 45, (size_t)(n + 1) * 4, &boff)) ||
+        (rc = scratch(ctx, 46, (size_t)n * 4, &bfill)) || (rc = scratch(ctx, 47, (size_t)n * 4, &blist)) ||
+        (rc = scratch(ctx, 48, (size_t)n * 4, &bind)) || (rc = scratch(ctx, 49, (size_t)n * 4, &bind2)) ||
+        (rc = scratch(ctx, 50, (size_t)n * 4, &bxv)) || (rc = scratch(ctx, 51, (size_t)n * 4, &bsl)) ||
+        (rc = scratch(ctx, 52, (size_t)n * 4, &bsr)) ||
+        (rc = scratch(ctx, 53, (size_t)trees * nodes_per_tree * 16, &bnodes)) ||
+        (rc = scratch(ctx, 54, (size_t)2 * n * 16, &bopen)) || (rc = scratch(ctx, 55, (size_t)(n + 2) * 4, &blev)) ||
+        (rc = scratch(ctx, 56, (size_t)nq * k * 4, &bidx)) || (rc = scratch(ctx, 57, (size_t)nq * k * 4, &bdist)) ||
+        (rc = scratch(ctx, 58, (size_t)nq * 4, &bflag)) || (rc = scratch(ctx, 59, (size_t)(nq + 1) * 4, &bredo)))
+        return rc;
+    hipStream_t s = ctx->stream;
+    Staging st;
+    if ((rc = staging(ctx, Staging::round((size_t)nq * dim * 4) + Staging::round((size_t)nt * dim * 4) +
+                               Staging::round((size_t)trees * kChunks * 8) + 2 * Staging::round((size_t)nq * k * 4) +
+                               2 * Staging::round(4),
+                      s, &st)))
+        return rc;
+    // the multiply-with-carry state at the start of every draw chunk of every tree (tree t's draws
+    // begin t (2n - 1) steps after the call's state)
+    std::vector<uint64_t> cs((size_t)trees * kChunks);
+    for (int t = 0; t < trees; ++t)
+        for (int c = 0; c < kChunks; ++c)
+            cs[(size_t)t * kChunks + c] =
+                therng_jump(*rng_state, (uint64_t)t * draws + (uint64_t)((int64_t)draws * c / kChunks));
+    HIP_TRY(st.put(bq, dq, (size_t)nq * dim * 4));
+    HIP_TRY(st.put(bt, dt, (size_t)nt * dim * 4));
+    HIP_TRY(st.put(bcs, cs.data(), cs.size() * 8));
+    // ind = 0..n-1 once; every tree shuffles the previous tree's final order (KDTreeIndex::buildIndex)
+    {
+        std::vector<int32_t> iota(n);
+        for (int i = 0; i < n; ++i) iota[i] = i;
+        HIP_TRY(hipMemcpyAsync(bind, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));  // the pageable copy must finish before iota goes out of scope
+    }
+    int* ind = (int*)bind;
+    int* ind2 = (int*)bind2;
+    int32_t* hcnt = reinterpret_cast<int32_t*>(st.take(4));
+    for (int t = 0; t < trees; ++t) {
+        HIP_TRY(launch_flann_draws((const uint64_t*)bcs + (size_t)t * kChunks, kChunks, draws, (uint32_t*)bR, s));
+        HIP_TRY(launch_flann_shuffle((const uint32_t*)bR, n, (int*)bcnt, (int*)boff, (int*)bfill, (int*)blist, ind, ind2,
+                                     s));
+        std::swap(ind, ind2);
+        FlannBuildArgs a{(const float*)bt, n, dim, ind, (float*)bxv, (int*)bsl, (int*)bsr, (const uint32_t*)bR,
+                         (int4*)bnodes + (size_t)t * nodes_per_tree, (int4*)bopen, (int4*)bopen + n, (int*)blev};
+        HIP_TRY(hipMemsetAsync(blev, 0, (size_t)(n + 2) * 4, s));
+        HIP_TRY(launch_flann_root(a, s));
+        // level-synchronous divideTree: a level has at most min(2^d, n / 2) open nodes; levels go in
+        // batches of 8, then the host reads whether the next level has any
+        for (int d = 0; d < n; d += 8) {
+            for (int e = d; e < d + 8 && e < n; ++e)
+                HIP_TRY(launch_flann_level(a, e, (int)std::min<int64_t>(int64_t(1) << std::min(e, 20), n / 2 + 1), s));
+            HIP_TRY(hipMemcpyAsync(hcnt, (int*)blev + std::min(d + 8, n + 1), 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (*hcnt == 0) break;
+        }
+    }
+    FlannSearchArgs sa{(const float*)bq, (const float*)bt, (const int4*)bnodes, nq, n, dim, k, trees, checks,
+                       (int32_t*)bidx, (float*)bdist, (int32_t*)bflag};
+    HIP_TRY(launch_flann_search(sa, s));
+    HIP_TRY(launch_flann_redo_list((const int32_t*)bflag, nq, (int32_t*)bredo + 1, (int32_t*)bredo, s));
+    int32_t* hredo = reinterpret_cast<int32_t*>(st.take(4));
+    HIP_TRY(hipMemcpyAsync(hredo, bredo, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int done = 0; done < *hredo;) {  // queries whose heap outgrew LDS, with the heap in global memory
+        const int batch = std::min(*hredo - done, 256);
+        void *bhd, *bhn;
+        if ((rc = scratch(ctx, 60, (size_t)batch * n * 4, &bhd)) || (rc = scratch(ctx, 61, (size_t)batch * n * 4, &bhn)))
+            return rc;
+        HIP_TRY(launch_flann_search_global(sa, (const int32_t*)bredo + 1 + done, batch, (float*)bhd, (int32_t*)bhn, s));
+        done += batch;
+    }
+    uint8_t *hi, *hd;
+    HIP_TRY(st.get(bidx, (size_t)nq * k * 4, &hi));
+    HIP_TRY(st.get(bdist, (size_t)nq * k * 4, &hd));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(train_idx, hi, (size_t)nq * k * 4);
+    std::memcpy(dist, hd, (size_t)nq * k * 4);
+    *rng_state = therng_jump(*rng_state, (uint64_t)trees * draws);
+    return DVO_OK;
+}
+
+namespace {
 // getGaussianKernel(ksize = cvRound(sigma * 8 + 1) | 1, sigma, CV_32F), as oracle/sift.cpp gauss_kernel
 std::vector<float> sift_gauss_taps(double sigma) {
     const int n = (int)std::nearbyint(sigma * 4 * 2 + 1) | 1;

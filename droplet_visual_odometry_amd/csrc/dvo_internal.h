@@ -323,6 +323,39 @@ hipError_t launch_sift(const SiftArgs& A, const uint8_t* d_img, int w, int h, in
 hipError_t launch_surf(const SurfArgs& a, hipStream_t s);
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s);
+// FLANN randomized kd-tree k-NN (flann.hip; the 'flann' mode's FlannBasedMatcher).
+struct FlannBuildArgs {
+    const float* data;  // train set [n][dim]
+    int n, dim;
+    int* ind;           // [n]
+    float* xv;          // [n]
+    int* sl;            // [n]
+    int* sr;            // [n]
+    const uint32_t* R;  // [2n - 1] draws of the tree
+    int4* nodes;        // [2n - 1] nodes of the tree
+    int4* open0;        // [n] open nodes, even levels
+    int4* open1;        // [n] open nodes, odd levels
+    int* cnt;           // [n + 2] open nodes per level
+};
+struct FlannSearchArgs {
+    const float* q;
+    const float* t;
+    const int4* nodes;  // [trees][2n - 1]
+    int nq, n, dim, k, trees, checks;
+    int32_t* idx;       // [nq][k]
+    float* dist;        // [nq][k] squared L2
+    int32_t* flag;      // [nq]
+};
+size_t flann_search_lds(int n);
+hipError_t launch_flann_draws(const uint64_t* d_chunk_state, int nchunk, int total, uint32_t* d_R, hipStream_t s);
+hipError_t launch_flann_shuffle(const uint32_t* d_R, int n, int* d_cnt, int* d_off, int* d_fill, int* d_list,
+                                const int* d_ind, int* d_new_ind, hipStream_t s);
+hipError_t launch_flann_root(const FlannBuildArgs& a, hipStream_t s);
+hipError_t launch_flann_level(const FlannBuildArgs& a, int level, int max_open, hipStream_t s);
+hipError_t launch_flann_search(const FlannSearchArgs& a, hipStream_t s);
+hipError_t launch_flann_redo_list(const int32_t* d_flag, int nq, int32_t* d_list, int32_t* d_count, hipStream_t s);
+hipError_t launch_flann_search_global(const FlannSearchArgs& a, const int32_t* d_list, int count, float* d_heap_d,
+                                      int32_t* d_heap_n, hipStream_t s);
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
                                    int semantics, int* d_k, hipStream_t s);
 hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int model_points, int max_iters,

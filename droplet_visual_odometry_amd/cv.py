@@ -307,26 +307,64 @@ class BFMatcher:
         return [r for r in out if r] if compactResult else out
 
 
+# cv::theRNG(): per-thread process state in OpenCV.  FLANN's kd-tree builds draw
+# from it (every FlannBasedMatcher.knnMatch builds an index), so the stand-in
+# carries it across calls the same way (cv2.setRNGSeed resets it).
+import threading as _threading
+
+_rng_tls = _threading.local()
+
+
+def _the_rng():
+    st = getattr(_rng_tls, "state", None)
+    return ops.THE_RNG_SEED if st is None else st
+
+
+def setRNGSeed(seed):
+    """cv2.setRNGSeed(int): theRNG() = RNG((uint64)seed); RNG(0) starts at 0xFFFFFFFF."""
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    _rng_tls.state = seed if seed else ops.THE_RNG_SEED
+
+
 class FlannBasedMatcher:
     """cv2.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50)) as
-    built at v3:206-212.  Served by EXACT k-nearest-neighbour search in FLANN's
-    distance (squared L2): FLANN's randomized kd-trees return the same
-    neighbours whenever their approximate search finds the true ones; where it
-    misses (seed dependent in OpenCV) the results differ — a documented
-    deviation (DESIGN.md row f).  DMatch.distance is sqrt(float32) of the
-    squared distance, as OpenCV's FlannBasedMatcher::convertToDMatches does
-    for float descriptors, so the 0.75 ratio test (v3:227) compares distances,
-    not their squares."""
+    built at v3:206-212: OpenCV's randomized kd-forest (FLANN_INDEX_KDTREE)
+    built over the train descriptors and searched approximately with `checks`
+    leaf visits, on the GPU (ops.flann_knn / dvo_flann_knn; oracle/flann.cpp
+    restates it).  The trees come from cv::theRNG(), carried per thread across
+    calls as in OpenCV.  DMatch.distance is sqrt(float32) of FLANN's squared
+    L2 distance, as FlannBasedMatcher::convertToDMatches does for float
+    descriptors, so the 0.75 ratio test (v3:227) compares distances."""
 
     def __init__(self, indexParams=None, searchParams=None):
         self.indexParams = dict(indexParams or {})
         self.searchParams = dict(searchParams or {})
+        if self.indexParams.get("algorithm", 1) != 1:
+            raise error("only FLANN_INDEX_KDTREE (algorithm=1) is implemented (the reference's choice, v3:207)")
+        self.trees = int(self.indexParams.get("trees", 4))        # KDTreeIndexParams default
+        self.checks = int(self.searchParams.get("checks", 32))    # SearchParams default
+        if float(self.searchParams.get("eps", 0.0)) != 0.0 or self.checks < 1:
+            raise error("only eps=0 and checks >= 1 are implemented")
 
     def knnMatch(self, queryDescriptors, trainDescriptors, k, mask=None, compactResult=False):
         if mask is not None:
             raise error("match masks are not supported")
-        out = _knn_lists(_float_desc(queryDescriptors), _float_desc(trainDescriptors), int(k), ops.NORM_L2SQR,
-                         sqrt_dist=True)
+        q, t = _float_desc(queryDescriptors), _float_desc(trainDescriptors)
+        if len(q) == 0 or len(t) == 0:  # DescriptorMatcher::knnMatch returns before training
+            return []
+        if q.shape[1] != t.shape[1]:
+            raise error("(-215:Assertion failed) query and train descriptors differ in length")
+        if int(k) > len(t):
+            raise error("(-215:Assertion failed) (size_t)knn <= index_->size() in function 'runKnnSearch_'")
+        try:
+            idx, dist, st = ops.flann_knn(q, t, int(k), self.trees, self.checks, _the_rng())
+        except DVOError as e:
+            raise error(str(e)) from e
+        _rng_tls.state = st
+        dist = np.sqrt(dist.astype(np.float32))
+        out = []
+        for qi in range(len(q)):
+            out.append([DMatch(qi, int(idx[qi, s]), 0, float(dist[qi, s])) for s in range(int(k)) if idx[qi, s] >= 0])
         return [r for r in out if r] if compactResult else out
 
 

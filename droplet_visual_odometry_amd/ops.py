@@ -128,6 +128,29 @@ def bf_knn_float(dq: np.ndarray, dt: np.ndarray, k: int = 2, norm: int = NORM_L1
     return idx[:nq].copy(), dist[:nq].copy()
 
 
+THE_RNG_SEED = 0xFFFFFFFF  # cv::theRNG() of a fresh thread (cv::RNG() state)
+
+
+def flann_knn(dq: np.ndarray, dt: np.ndarray, k: int = 2, trees: int = 5, checks: int = 50,
+              rng_state: int = THE_RNG_SEED, ctx=None):
+    """FlannBasedMatcher(KDTREE trees, checks).knnMatch(dq, dt, k) on the GPU
+    (dvo_flann_knn): (train_idx int32[nq, k], squared L2 float32[nq, k], the
+    cv::theRNG() state after the call).  The randomized kd-forest and its
+    approximate search reproduce OpenCV's, given the theRNG state before."""
+    c = _ctx(ctx)
+    dq = np.ascontiguousarray(dq, np.float32)
+    dt = np.ascontiguousarray(dt, np.float32)
+    if dq.ndim != 2 or dt.ndim != 2 or (len(dt) and len(dq) and dt.shape[1] != dq.shape[1]):
+        raise DVOError(-1, "descriptors must be float32[n, dim] with the same dim")
+    nq, nt, dim = dq.shape[0], dt.shape[0], dq.shape[1] if dq.size else dt.shape[1]
+    idx = np.zeros((max(nq, 1), k), np.int32)
+    dist = np.zeros((max(nq, 1), k), np.float32)
+    st = ctypes.c_uint64(int(rng_state))
+    c.check(c.lib.dvo_flann_knn(c.h, ptr(dq), nq, ptr(dt), nt, dim, int(k), int(trees), int(checks), ctypes.byref(st),
+                                ptr(idx), ptr(dist)))
+    return idx[:nq].copy(), dist[:nq].copy(), int(st.value)
+
+
 def _pts(p):
     p = np.ascontiguousarray(np.asarray(p, dtype=np.float64).reshape(-1, 2))
     return p

@@ -103,6 +103,23 @@ int dvo_bf_match_hamming(dvo_ctx* ctx, const uint8_t* dq, int nq, const uint8_t*
 int dvo_bf_knn_float(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
                      int32_t* train_idx, float* dist);
 
+/* Replaces cv::FlannBasedMatcher(dict(algorithm=FLANN_INDEX_KDTREE, trees),
+ * dict(checks)).knnMatch(query, train, k) on float descriptors — the 'flann'
+ * mode, visual_odometry_v3.py:206-212 (trees 5, checks 50, k 2), whose ratio
+ * test follows at :223-228.  OpenCV's randomized kd-forest (FLANN 1.6 as
+ * bundled with OpenCV 4.x, restated in oracle/flann.cpp) is built over the
+ * train set and searched approximately, on the device: the same trees, the
+ * same visiting order, the same neighbours.  The trees are drawn from
+ * cv::theRNG(), process state in the reference; *rng_state carries it: the
+ * state before the call on entry (a fresh thread's is 0xFFFFFFFF) and after
+ * it on return (advanced trees * (2 nt - 1) draws).  dist: squared L2 (as
+ * FLANN reports it; FlannBasedMatcher returns its square root); per query k
+ * entries ascending by (distance, train index).  dim a multiple of 4 up to
+ * 256, k <= nt (else DVO_EINVAL, where FLANN asserts), nt <= 65536.  An empty
+ * query or train set returns at once without touching the state. */
+int dvo_flann_knn(dvo_ctx* ctx, const float* dq, int nq, const float* dt, int nt, int dim, int k, int trees,
+                  int checks, uint64_t* rng_state, int32_t* train_idx, float* dist);
+
 /* Replaces cv::xfeatures2d::SIFT_create().detectAndCompute(img, None) — the
  * detector of the 'sift' / 'knn_sift' / 'flann' modes, visual_odometry_v3.py:100
  * (construction) and :373 (call).  Default parameters (nfeatures 0, 3 octave

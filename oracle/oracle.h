@@ -68,6 +68,15 @@ int ora_bf_match_hamming(const uint8_t* dq, int nq, const uint8_t* dt, int nt,
 int ora_bf_knn_float(const float* dq, int nq, const float* dt, int nt, int dim, int k, int norm,
                      int32_t* tidx, float* dist);
 
+// ---- FlannBasedMatcher(KDTREE trees, checks).knnMatch on float descriptors
+// (flann.cpp; the 'flann' mode, visual_odometry_v3.py:206-212): index over the
+// train set, squared L2 distances, k smallest (distance, index) among the
+// checked points.  rng_state: cv::theRNG() state before (in) / after (out).
+// -1 on bad arguments (OpenCV asserts k <= train size).
+int ora_flann_knn(const float* dq, int nq, const float* dt, int nt, int dim, int k, int trees, int checks,
+                  uint64_t* rng_state, int32_t* tidx, float* dist);
+uint64_t ora_flann_rng_after(uint64_t state, const int32_t* n, int calls, int trees);
+
 // ---- findEssentialMat(RANSAC) / recoverPose / triangulatePoints -------------
 // E_out holds up to 10 stacked 3x3 models (only when m == 5); *rows = 3*k.
 // Returns 0 on success, <0 on failure (E empty).

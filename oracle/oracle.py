@@ -90,6 +90,7 @@ def lib():
             "ora_retain_best_depth_v": [_f32p, _c, _c, _c, _c, _i32p],
             "ora_bf_match_hamming": [_u8p, _c, _u8p, _c, _c, _i32p, _i32p, _f32p, _ip],
             "ora_bf_knn_float": [_f32p, _c, _f32p, _c, _c, _c, _c, _i32p, _f32p],
+            "ora_flann_knn": [_f32p, _c, _f32p, _c, _c, _c, _c, _c, ctypes.POINTER(ctypes.c_uint64), _i32p, _f32p],
             "ora_find_essential": [_f64p, _f64p, _c, _f64p, _d, _d, _c, _f64p, _ip, _u8p, _ip],
             "ora_recover_pose": [_f64p, _f64p, _f64p, _c, _f64p, _d, ctypes.c_void_p, _f64p, _f64p, _u8p, _ip],
             "ora_triangulate": [_f64p, _f64p, _f64p, _f64p, _c, _f64p],
@@ -109,6 +110,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
+        L.ora_flann_rng_after.argtypes = [ctypes.c_uint64, _i32p, _c, _c]
+        L.ora_flann_rng_after.restype = ctypes.c_uint64
         _lib = L
     return _lib
 
@@ -421,3 +424,28 @@ def undistort(img, K, dist, newK=None):
     if rc:
         raise ValueError("singular new camera matrix")
     return dst, xy, fr
+
+
+THE_RNG_SEED = 0xFFFFFFFF  # cv::theRNG() of a fresh thread (RNG() state)
+
+
+def flann_knn(dq, dt, k=2, trees=5, checks=50, rng_state=THE_RNG_SEED):
+    """FlannBasedMatcher(KDTREE, trees).knnMatch(dq, dt, k) with search checks
+    (flann.cpp): (train_idx int32[nq, k], squared distances float32[nq, k],
+    the theRNG state after the call)."""
+    dq = np.ascontiguousarray(dq, np.float32)
+    dt = np.ascontiguousarray(dt, np.float32)
+    nq, dim = dq.shape
+    idx = np.zeros((max(nq, 1), k), np.int32)
+    dist = np.zeros((max(nq, 1), k), np.float32)
+    st = ctypes.c_uint64(rng_state)
+    rc = lib().ora_flann_knn(dq.reshape(-1) if nq else np.zeros(dim, np.float32), nq, dt.reshape(-1), len(dt), dim,
+                             k, trees, checks, ctypes.byref(st), idx, dist)
+    if rc:
+        raise ValueError("flann_knn: bad arguments (k must not exceed the train set)")
+    return idx[:nq], dist[:nq], st.value
+
+
+def flann_rng_after(state, train_sizes, trees=5):
+    n = np.ascontiguousarray(train_sizes, np.int32)
+    return int(lib().ora_flann_rng_after(state, n, len(n), trees))

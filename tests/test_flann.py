@@ -1,0 +1,165 @@
+"""FLANN randomized kd-forest k-NN: the matcher of the reference's 'flann'
+mode, cv.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50))
+.knnMatch(previous, current, k=2) (scripts/visual_odometry_v3.py:206-212).
+
+CPU: the oracle restatement (oracle/flann.cpp) -- its theRNG bookkeeping,
+determinism, and the size of its deviation from exact search on the synthetic
+SIFT stream (why the GPU builds the same trees instead of searching exactly).
+GPU: dvo_flann_knn bit-exact against the oracle (indices and squared
+distances), including the theRNG state carried across calls, ties, tiny train
+sets, non-integer descriptors and the global-memory heap path.
+
+Parity against OpenCV's own FLANN is unpinned: no cv2 here; the restatement
+follows OpenCV 4.x's bundled FLANN 1.6 (see oracle/flann.cpp)."""
+import numpy as np
+import pytest
+
+from conftest import synth_frames
+
+
+def _sift_pair(oracle_mod, i=0, W=640, H=480):
+    fr, K = synth_frames(W, H, [i, i + 1])
+    return oracle_mod.sift_detect_and_compute(fr[0]), oracle_mod.sift_detect_and_compute(fr[1]), K
+
+
+def test_oracle_rng_bookkeeping(oracle_mod):
+    """Every call draws trees x (2 n - 1) theRNG values (n shuffle draws and one
+    per internal node), whatever the data; results depend on the state."""
+    rng = np.random.default_rng(0)
+    q = rng.integers(0, 256, (40, 128)).astype(np.float32)
+    st = oracle_mod.THE_RNG_SEED
+    outs = []
+    for n in (1, 2, 7, 300):
+        t = rng.integers(0, 256, (n, 128)).astype(np.float32)
+        idx, dist, st2 = oracle_mod.flann_knn(q, t, 1, trees=5, checks=50, rng_state=st)
+        assert st2 == oracle_mod.flann_rng_after(st, [n], trees=5)
+        again = oracle_mod.flann_knn(q, t, 1, trees=5, checks=50, rng_state=st)
+        np.testing.assert_array_equal(again[0], idx)
+        outs.append((t, idx))
+        st = st2
+    t, idx = outs[-1]
+    other = oracle_mod.flann_knn(q, t, 1, trees=5, checks=50, rng_state=12345)[0]
+    assert not np.array_equal(other, idx)  # another state, other trees, other approximate answers
+
+
+def test_oracle_tiny_train_sets_are_exact(oracle_mod):
+    """With at most `checks` train points every leaf is checked: the answer is
+    the exact k-NN in (distance, index) order."""
+    rng = np.random.default_rng(1)
+    q = rng.integers(0, 256, (50, 64)).astype(np.float32)
+    for n in (2, 3, 10, 49):
+        t = rng.integers(0, 256, (n, 64)).astype(np.float32)
+        idx, dist, _ = oracle_mod.flann_knn(q, t, 2, trees=5, checks=50)
+        ei, ed = oracle_mod.bf_knn_float(q, t, 2, 1)
+        np.testing.assert_array_equal(idx, ei)
+        np.testing.assert_array_equal(dist, ed)
+
+
+def test_oracle_deviation_from_exact_search(oracle_mod):
+    """The reason the flann mode needs the real kd-forest: on the synthetic SIFT
+    stream the approximate search (checks = 50) misses the exact nearest
+    neighbours often enough that the 0.75 ratio-test survivors differ and so
+    does every E (RANSAC samples positions of the survivor list)."""
+    st = oracle_mod.THE_RNG_SEED
+    agree = total = e_same = 0
+    for i in range(2):
+        (k0, d0), (k1, d1), K = _sift_pair(oracle_mod, i)
+        fi, fd, st = oracle_mod.flann_knn(d0, d1, 2, rng_state=st)
+        ei, ed = oracle_mod.bf_knn_float(d0, d1, 2, 1)
+
+        def surv(idx, dd):
+            dd = np.sqrt(dd.astype(np.float32))
+            return [(q, int(idx[q, 0])) for q in range(len(idx)) if dd[q, 0] < 0.75 * dd[q, 1]]
+        sf, se = surv(fi, fd), surv(ei, ed)
+        agree += len(set(sf) & set(se))
+        total += len(se)
+        assert (fi[:, 0] != ei[:, 0]).mean() > 0.05  # > 5 % of first neighbours differ
+
+        def E_of(s):
+            p1 = np.array([[k0[q]["x"], k0[q]["y"]] for q, _ in s], np.float64)
+            p2 = np.array([[k1[t]["x"], k1[t]["y"]] for _, t in s], np.float64)
+            return oracle_mod.find_essential(p1, p2, K)[0]
+        e_same += np.array_equal(E_of(sf), E_of(se))
+    assert 0.9 < agree / total < 1.0
+    assert e_same == 0
+
+
+# ---------------------------------------------------------------- GPU parity
+def _gpu_vs_oracle(gpu_ctx, oracle_mod, q, t, k=2, trees=5, checks=50, state=None):
+    from droplet_visual_odometry_amd import ops
+    state = oracle_mod.THE_RNG_SEED if state is None else state
+    gi, gd, gs = ops.flann_knn(q, t, k, trees, checks, state, ctx=gpu_ctx)
+    oi, od, os_ = oracle_mod.flann_knn(q, t, k, trees=trees, checks=checks, rng_state=state)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd, od)
+    assert gs == os_
+    return gs
+
+
+@pytest.mark.gpu
+def test_gpu_flann_sift_stream(gpu_ctx, oracle_mod):
+    """The reference's call on consecutive SIFT pairs, theRNG state chained."""
+    st = None
+    for i in range(3):
+        (_, d0), (_, d1), _ = _sift_pair(oracle_mod, i)
+        st = _gpu_vs_oracle(gpu_ctx, oracle_mod, d0, d1, state=st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,dim,k,trees,checks", [
+    (1, 128, 1, 5, 50), (2, 128, 2, 5, 50), (5, 64, 4, 3, 1), (257, 128, 2, 1, 50), (3000, 128, 2, 5, 50),
+    (3000, 64, 3, 8, 200), (1500, 128, 2, 5, 1),
+])
+def test_gpu_flann_shapes(gpu_ctx, oracle_mod, n, dim, k, trees, checks):
+    rng = np.random.default_rng(n + dim)
+    t = rng.integers(0, 256, (n, dim)).astype(np.float32)
+    q = np.clip(np.concatenate([t[: min(n, 400)] + rng.integers(-6, 7, (min(n, 400), dim)),
+                                rng.integers(0, 256, (300, dim))]), 0, 255).astype(np.float32)
+    _gpu_vs_oracle(gpu_ctx, oracle_mod, q, t, k, trees, checks, state=0x1234567 + n)
+
+
+@pytest.mark.gpu
+def test_gpu_flann_ties_and_duplicates(gpu_ctx, oracle_mod):
+    """Repeated train rows and values (equal variances, equal split values,
+    equal distances): the split rule's lim1 / lim2 cases and the (distance,
+    index) order of the result set."""
+    rng = np.random.default_rng(5)
+    base = rng.integers(0, 4, (200, 128)).astype(np.float32)
+    t = np.concatenate([base, base, base[:50], np.zeros((30, 128), np.float32)])
+    q = np.concatenate([base[:100], rng.integers(0, 4, (100, 128)).astype(np.float32)])
+    _gpu_vs_oracle(gpu_ctx, oracle_mod, q, t, k=4, trees=5, checks=50)
+
+
+@pytest.mark.gpu
+def test_gpu_flann_non_integer_descriptors(gpu_ctx, oracle_mod):
+    """Real-valued (SURF-like) rows: float sums in flann::L2's grouped order,
+    means and variances in point order."""
+    rng = np.random.default_rng(9)
+    t = rng.standard_normal((2000, 64)).astype(np.float32)
+    q = (t[:500] + 0.05 * rng.standard_normal((500, 64))).astype(np.float32)
+    _gpu_vs_oracle(gpu_ctx, oracle_mod, q, t, k=2, trees=5, checks=50)
+
+
+@pytest.mark.gpu
+def test_gpu_flann_global_heap_path(gpu_ctx, oracle_mod):
+    """A large `checks` makes branch heaps outgrow the 1024 LDS entries: those
+    queries are redone with the heap in global memory, same answers."""
+    rng = np.random.default_rng(3)
+    t = rng.integers(0, 256, (6000, 128)).astype(np.float32)
+    q = rng.integers(0, 256, (64, 128)).astype(np.float32)
+    _gpu_vs_oracle(gpu_ctx, oracle_mod, q, t, k=2, trees=5, checks=4000)
+
+
+@pytest.mark.gpu
+def test_gpu_flann_errors_and_empty(gpu_ctx, oracle_mod):
+    from droplet_visual_odometry_amd import cv, ops
+    from droplet_visual_odometry_amd._native import DVOError
+    t = np.ones((3, 128), np.float32)
+    with pytest.raises(DVOError):
+        ops.flann_knn(np.ones((2, 128), np.float32), t, k=4, ctx=gpu_ctx)  # knn > index size: FLANN asserts
+    idx, dist, st = ops.flann_knn(np.zeros((0, 128), np.float32), t, 2, ctx=gpu_ctx)
+    assert idx.shape == (0, 2) and st == ops.THE_RNG_SEED  # no training on an empty query: theRNG untouched
+    m = cv.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50))
+    with pytest.raises(cv.error):
+        m.knnMatch(np.ones((2, 128), np.float32), t, k=4)
+    assert m.knnMatch(np.zeros((0, 128), np.float32), t, k=2) == []

@@ -68,7 +68,8 @@ def _yaml(K):
 @pytest.mark.parametrize("mode", ["knn_sift", "flann"])
 def test_dropin_sift_modes_end_to_end(gpu_ctx, oracle_mod, tmp_path, mode):
     """visual_odometry_calculations in the k-NN SIFT modes: SIFT on both
-    frames, knnMatch(k=2) (BFMatcher L1 or the FLANN stand-in), the 0.75 ratio
+    frames, knnMatch(k=2) (BFMatcher L1 or the FLANN kd-forest, its theRNG
+    state carried from pair to pair), the 0.75 ratio
     test (v3:223-228), findEssentialMat / recoverPose on the kept keypoints;
     E bit-identical to the oracle run of the same chain."""
     from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
@@ -82,14 +83,19 @@ def test_dropin_sift_modes_end_to_end(gpu_ctx, oracle_mod, tmp_path, mode):
     y.write_text(_yaml(K))
     vo = v3.VisualOdometry(mode=mode, calibration_file_path=str(y), controlled=True, real_marker_length=MARKER_LEN)
     T = vo.robot_curr_position
+    from droplet_visual_odometry_amd import cv
+    cv.setRNGSeed(0)  # the harness process's cv::theRNG(), carried across the pairs
+    state = oracle_mod.THE_RNG_SEED
     for i in range(2):
         T, rel = vo.visual_odometry_calculations(frames[i], frames[i + 1], T, marker_corners(i, K),
                                                  marker_corners(i + 1, K))
         k1, d1 = oracle_mod.sift_detect_and_compute(frames[i])
         k2, d2 = oracle_mod.sift_detect_and_compute(frames[i + 1])
-        idx, dist = oracle_mod.bf_knn_float(d1, d2, 2, 1 if mode == "flann" else 0)
         if mode == "flann":
+            idx, dist, state = oracle_mod.flann_knn(d1, d2, 2, trees=5, checks=50, rng_state=state)
             dist = np.sqrt(dist.astype(np.float32))
+        else:
+            idx, dist = oracle_mod.bf_knn_float(d1, d2, 2, 0)
         keep = [q for q in range(len(d1)) if float(dist[q, 0]) < 0.75 * float(dist[q, 1])]
         p1 = np.stack([k1["x"][keep], k1["y"][keep]], 1).astype(np.float64)
         p2 = np.stack([k2["x"][idx[keep, 0]], k2["y"][idx[keep, 0]]], 1).astype(np.float64)

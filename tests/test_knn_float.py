@@ -159,7 +159,8 @@ def test_cv_matchers_and_ratio_modes(gpu_ctx, oracle_mod):
     passed = [[m] for m, n in knn if m.distance < 0.75 * n.distance]
     expect = [q for q in range(600) if float(d_o[q, 0]) < 0.75 * float(d_o[q, 1])]
     assert [p[0].queryIdx for p in passed] == expect and len(expect) >= 350
-    i_f, d_f = oracle_mod.bf_knn_float(prev, cur, 2, 1)
+    cv.setRNGSeed(0)  # a fresh thread's cv::theRNG()
+    i_f, d_f, _ = oracle_mod.flann_knn(prev, cur, 2, trees=5, checks=50)
     fl = cv.FlannBasedMatcher(dict(algorithm=1, trees=5), dict(checks=50)).knnMatch(prev, cur, k=2)
     # DMatch.distance = std::sqrt(float squared-L2), FlannBasedMatcher::convertToDMatches
     s_f = np.sqrt(d_f.astype(np.float32))
@@ -194,10 +195,13 @@ def test_dropin_ratio_modes(gpu_ctx, oracle_mod, mode):
     kp_prev = [cv.KeyPoint(float(i), 0.0) for i in range(300)]
     kp_cur = [cv.KeyPoint(float(i), 1.0) for i in range(350)]
     me = types.SimpleNamespace(mode=mode, bf=cv.BFMatcher(normType=cv.NORM_L1, crossCheck=False))
+    cv.setRNGSeed(0)
     matches, top_prev, top_cur = v3.VisualOdometry.get_matches_between_two_frames(me, kp_prev, prev, kp_cur, cur)
-    idx, dist = oracle_mod.bf_knn_float(prev, cur, 2, 1 if mode == "flann" else 0)
     if mode == "flann":  # FLANN's DMatch.distance is sqrt(float) of the squared L2 distance
+        idx, dist, _ = oracle_mod.flann_knn(prev, cur, 2, trees=5, checks=50)
         dist = np.sqrt(dist.astype(np.float32))
+    else:
+        idx, dist = oracle_mod.bf_knn_float(prev, cur, 2, 0)
     keep = [q for q in range(300) if float(dist[q, 0]) < 0.75 * float(dist[q, 1])]
     assert len(matches) == 300 and len(keep) >= 150
     assert [kp.pt[0] for kp in top_prev] == [float(q) for q in keep]

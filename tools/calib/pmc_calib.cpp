@@ -44,9 +44,28 @@ __global__ __launch_bounds__(kNT) void calib_read_b128_global(const uint4* src, 
     if (acc == 0x12345678u) sink[blockIdx.x] = acc;
 }
 
+// (acc stays below 256, so the sink test must be a byte value or the compiler drops the loads:
+// round 2's b8 reading of 4 KB per GiB was that)
 __global__ __launch_bounds__(kNT) void calib_read_b8_global(const uint8_t* src, uint32_t* sink) {
     uint32_t acc = 0;
     for (size_t i = blockIdx.x * (size_t)kNT + threadIdx.x; i < kBytes; i += (size_t)gridDim.x * kNT) acc ^= src[i];
+    if (acc == 0x5Au) sink[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kNT) void calib_read_b32_global(const uint32_t* src, uint32_t* sink) {
+    uint32_t acc = 0;
+    const size_t n = kBytes / 4;
+    for (size_t i = blockIdx.x * (size_t)kNT + threadIdx.x; i < n; i += (size_t)gridDim.x * kNT) acc ^= src[i];
+    if (acc == 0x12345678u) sink[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kNT) void calib_read_b64_global(const uint2* src, uint32_t* sink) {
+    uint32_t acc = 0;
+    const size_t n = kBytes / 8;
+    for (size_t i = blockIdx.x * (size_t)kNT + threadIdx.x; i < n; i += (size_t)gridDim.x * kNT) {
+        const uint2 v = src[i];
+        acc ^= v.x ^ v.y;
+    }
     if (acc == 0x12345678u) sink[blockIdx.x] = acc;
 }
 
@@ -90,13 +109,16 @@ int main() {
     hipLaunchKernelGGL(calib_write_b128_global, dim3(grid), dim3(kNT), 0, 0, (uint4*)buf[1]);
     hipLaunchKernelGGL(calib_write_b8_global, dim3(grid), dim3(kNT), 0, 0, buf[2]);
     hipLaunchKernelGGL(calib_write_b32_global, dim3(grid), dim3(kNT), 0, 0, (uint32_t*)buf[0]);
+    hipLaunchKernelGGL(calib_read_b32_global, dim3(grid), dim3(kNT), 0, 0, (const uint32_t*)buf[1], sink);
+    hipLaunchKernelGGL(calib_read_b64_global, dim3(grid), dim3(kNT), 0, 0, (const uint2*)buf[2], sink);
     CHECK(hipGetLastError());
     CHECK(hipDeviceSynchronize());
     const char* names[] = {"calib_read_b32_buffer",  "calib_read_b128_global",  "calib_read_b8_global",
                            "calib_write_b32_buffer", "calib_write_b128_global", "calib_write_b8_global",
-                           "calib_write_b32_global"};
-    for (int i = 0; i < 7; ++i)
-        printf("{\"kernel\": \"%s\", \"%s_bytes\": %zu}\n", names[i], i < 3 ? "read" : "write", kBytes);
+                           "calib_write_b32_global", "calib_read_b32_global",   "calib_read_b64_global"};
+    for (int i = 0; i < 9; ++i)
+        printf("{\"kernel\": \"%s\", \"%s_bytes\": %zu}\n", names[i], names[i][6] == 'r' ? "read" : "write",
+               kBytes);
     for (auto& b : buf) CHECK(hipFree(b));
     CHECK(hipFree(sink));
     return 0;

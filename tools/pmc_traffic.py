@@ -27,8 +27,12 @@ def load(path, counters):
     return out
 
 
-def main(fetch, write, sq, calib, dst, batch=1024):
+RQ = ["TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_sum"]
+
+
+def main(fetch, write, sq, calib, dst, batch=1024, rdreq=None):
     f = load(fetch, ["FETCH_SIZE"])
+    rq = load(rdreq, RQ) if rdreq else {}
     w = load(write, ["WRITE_SIZE"])
     s = load(sq, ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD",
                   "SQ_INSTS_VMEM_WR", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"])
@@ -38,7 +42,15 @@ def main(fetch, write, sq, calib, dst, batch=1024):
         fr = f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024.0
         wr = w.get(k, {}).get("WRITE_SIZE", 0.0) * 1024.0
         e = {"fetch_bytes_raw": fr, "write_bytes_raw": wr}
-        if k in KERNEL_WIDTHS:
+        if k in rq:
+            # every kernel: the bytes of its read requests by size (32/64/128 B, gfx950 TCC_EA0_RDREQ_*B),
+            # checked on the known-bytes kernels (calibration read_requests); writes: WRITE_SIZE, exact for
+            # the calibrated store widths
+            r = rq[k]
+            fb = 32 * r.get(RQ[0], 0.0) + 64 * r.get(RQ[1], 0.0) + 128 * r.get(RQ[2], 0.0)
+            e.update(fetch_bytes=fb, write_bytes=wr, calibrated=True,
+                     widths={"read": "request sizes", "requests": r, "write": "WRITE_SIZE"})
+        elif k in KERNEL_WIDTHS:
             rw, ww = KERNEL_WIDTHS[k]
             fa, wa = cal["read"][rw]["factor"], cal["write"][ww]["factor"]
             e.update(fetch_bytes=fr * fa, write_bytes=wr * wa, calibrated=True,
@@ -54,10 +66,12 @@ def main(fetch, write, sq, calib, dst, batch=1024):
                 "SQ_* instruction counts (wave-level)",
         "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts), mean over dispatches",
         "calibration": os.path.basename(calib),
+        "read_bytes": "32 n32 + 64 n64 + 128 n128 from the TCC_EA0_RDREQ_*B pass" if rq else "FETCH_SIZE x width factor",
         "kernels": kernels,
     }
     json.dump(doc, open(dst, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    a = sys.argv[1:]
+    main(*a[:5], int(a[5]) if len(a) > 5 else 1024, a[6] if len(a) > 6 else None)

@@ -21,11 +21,19 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 60 rocprofv3 --pmc $c -d /tmp/cal_${tag}_$c -o run --output-format csv -- "$root/tools/calib/build/pmc_calib" > "$out/${tag}_calib_known.jsonl" 2> "$out/${tag}_calib_$c.log"
   python3 "$root/tools/pmc_summary.py" $(find /tmp/cal_${tag}_$c -name '*counter_collection.csv') "$out/${tag}_calib_$c.csv" > /dev/null
 done
+# read requests by size (gfx950 TCC_EA0_RDREQ_{32B,64B,128B}): the bytes every kernel fetched,
+# 32 n32 + 64 n64 + 128 n128, whatever its access widths (FETCH_SIZE tallies 128-B requests at 64 B
+# here); the calibration kernels check the decomposition against known byte counts
+rq="TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
+timeout -s KILL 320 rocprofv3 --pmc $rq -d /tmp/pmc_${tag}_rq -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_rdreq.log" 2>&1
+python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_rq -name '*counter_collection.csv') "$out/${tag}_pmc_rdreq.csv" > /dev/null
+timeout -s KILL 60 rocprofv3 --pmc $rq -d /tmp/cal_${tag}_rq -o run --output-format csv -- "$root/tools/calib/build/pmc_calib" > /dev/null 2> "$out/${tag}_calib_rdreq.log"
+python3 "$root/tools/pmc_summary.py" $(find /tmp/cal_${tag}_rq -name '*counter_collection.csv') "$out/${tag}_calib_rdreq.csv" > /dev/null
 timeout -s KILL 170 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
   -d /tmp/pmc_${tag}_sq -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_sq.log" 2>&1
 python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_sq -name '*counter_collection.csv') "$out/${tag}_pmc_sq.csv" > /dev/null
-python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" > /dev/null
-python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512
+python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_calib_rdreq.csv" > /dev/null
+python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512 "$out/${tag}_pmc_rdreq.csv"
 # stall breakdown (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES, MI355X_MICROARCH.md PMC slots)
 timeout -s KILL 170 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
   -d /tmp/pmc_${tag}_stall -o run --output-format csv -- python3 "$root/bench.py" $short > "$out/${tag}_pmc_stall.log" 2>&1 &&
