@@ -423,7 +423,6 @@ int stream_alloc(dvo_stream* s) {
     A(b.cnt2, (size_t)F * kMaxLevels);
     A(b.kps, (size_t)F * cap);
     A(b.desc, (size_t)F * cap * 32);
-    A(b.desc_x, (size_t)F * cap * 256);
     A(b.nkp, (size_t)F);
     A(b.nn, (size_t)2 * F * cap);
     A(b.mq, (size_t)F * cap);

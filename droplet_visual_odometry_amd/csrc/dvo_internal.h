@@ -115,8 +115,7 @@ struct Buffers {
     int32_t* cnt1;        // [F][8] after FAST retainBest
     int32_t* cnt2;        // [F][8] after Harris retainBest
     dvo_keypoint* kps;    // [F][kp_cap]
-    uint8_t* desc;        // [F][kp_cap][32]
-    int8_t* desc_x;       // [F][kp_cap][256]: descriptor bits as +-1 bytes (the matcher's MFMA operands)
+    uint8_t* desc;        // [F][kp_cap][32] (also the matcher's operands, expanded in registers)
     int32_t* nkp;         // [F]
     int32_t* nn;          // [2][F][kp_cap] packed (dist << 16 | idx), -1 none
     int32_t* mq;          // [F][kp_cap] match queryIdx (sorted by (dist, q))

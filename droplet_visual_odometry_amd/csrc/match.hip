@@ -6,7 +6,7 @@
 // (v3:355, v3:358).
 //
 // nn_mfma_kernel: forward and backward nearest neighbours of a pair on the
-// matrix cores (int8 MFMA over +-1 descriptor bytes), for the batched stream
+// matrix cores (int8 MFMA over descriptor bits expanded to +-64 bytes), for the batched stream
 // and, through a one-pair parameter block, for the per-call C-ABI.
 // crosscheck_*_kernel: mutual-NN filter, then a bitonic sort of the unique
 // keys (distance << 16 | queryIdx) in LDS, then the point gather.
@@ -20,31 +20,43 @@ namespace dvo {
 namespace {
 
 // Forward + backward nearest neighbours of one stream pair on the matrix cores.
-// Descriptor bits are +-1 bytes (desc_x, written by describe_kernel); scaled
-// on the way into registers / LDS to +64 (queries) and -64 (trains), the
+// The operands are the packed 32-byte descriptors (P.buf.desc, as described;
+// the per-call path's caller buffers), expanded in registers on the way in:
+// every descriptor bit becomes a byte, +64 on the query side and -64 on the
+// train side when set (the opposite sign when clear), so the
 // v_mfma_i32_32x32x32_i8 accumulator is D = -4096 s where s = q.t = 256 -
 // 2 * Hamming(q, t), exact in int32.  Then key = 2^20 + D + index =
 // Hamming * 8192 + index (index < 8192): one add per element and direction,
 // and the minimum key is OpenCV's nearest neighbour with its first-index tie
 // rule.  A wave owns 64 queries (two 32-row strips, A fragments resident in
-// VGPRs); the workgroup streams the trains through LDS 64 at a time, double-
-// buffered (the next stage's global loads are in flight during this stage's
-// MFMAs; one barrier per stage), 16-byte chunks XOR-swizzled by train so the
-// b128 fragment reads are conflict-free.  Forward keys fold into a per-
-// register running minimum (the lane's column changes, its rows do not);
-// backward keys fold over the lane's 32 rows (v_min3), into LDS, then a global
-// atomicMin per train in the (Hamming << 16 | index) form the cross check
-// reads (the re-encoding is monotone, so the minimum is the same).  Workgroups
-// are grouped by XCD (blocks b and b + 8 share one) so the query blocks of a
-// pair stream its trains through one L2.
+// VGPRs); the workgroup streams the trains through LDS 64 at a time (2 KB of
+// packed rows per stage, 16 KB expanded), double-buffered (the next stage's
+// global loads are in flight during this stage's MFMAs; one barrier per
+// stage), 16-byte chunks XOR-swizzled by train so the b128 fragment reads are
+// conflict-free.  Forward keys fold into a per-register running minimum (the
+// lane's column changes, its rows do not); backward keys fold over the lane's
+// 32 rows (v_min3), into LDS, then a global atomicMin per train in the
+// (Hamming << 16 | index) form the cross check reads (the re-encoding is
+// monotone, so the minimum is the same).  Workgroups are grouped by XCD
+// (blocks b and b + 8 share one) so the query blocks of a pair stream its
+// trains through one L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kMWaves = 4, kMQB = 64 * kMWaves, kMStage = 64;
 constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^22), < 0x7F7F7F7F
 constexpr int kKeyBase = 1 << 20;     // 256 * 4096
 
-__device__ __forceinline__ v4i scale_q(v4i x) { return (x & 0x03030303) << 6; }                 // +-1 -> +-64
-__device__ __forceinline__ v4i scale_t(v4i x) { return ((x & 0x03030303) << 6) ^ (int)0x80808080; }  // +-1 -> -+64
+// 16 descriptor bits (chunk c = bits 16c .. 16c+15 = packed bytes 2c, 2c+1) to
+// 16 bytes, byte j from bit j: (nibble * 0x204081) & 0x01010101 spreads a
+// nibble's bit i to byte i; base ^ (spread << 7) flips 0x40 <-> 0xC0 (+-64).
+// Query side base 0xC0C0C0C0 (set -> +64), train side 0x40404040 (set -> -64).
+__device__ __forceinline__ v4i expand16(uint32_t bits, uint32_t base) {
+    v4i r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = (int)(base ^ ((((bits >> (4 * k)) & 0xFu) * 0x00204081u & 0x01010101u) << 7));
+    return r;
+}
+constexpr uint32_t kExpQ = 0xC0C0C0C0u, kExpT = 0x40404040u;
 __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 8191); }
 
 template <bool kFull>
@@ -80,10 +92,20 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
     }
 }
 
+// Operands of one launch: pair p's queries are the rows at q0 + p * stride,
+// its trains the rows at t0 + p * stride (32 bytes each); counts from nkp[p],
+// nkp[p + 1] (the stream) or nq_fix / nt_fix (the per-call pair, >= 0).
+struct NnOperands {
+    const uint8_t* q0;
+    const uint8_t* t0;
+    int64_t stride;
+    int nq_fix, nt_fix;
+};
+
 // tsplit > 1 (the per-call path: one pair, so a short grid) gives each
 // workgroup a contiguous 1/tsplit of the train stages and folds the forward
 // keys with atomicMin too (fwd pre-filled with 0x7F7F7F7F).
-__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs, int nqb, int tsplit) {
+__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit) {
     __shared__ v4i bt[2][kMStage * 16];
     __shared__ int colmin[2][kMStage];
     const int nwg = gridDim.x;  // a multiple of 8
@@ -92,13 +114,14 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
     const int p = L / nqb, qb = L - p * nqb;
     if (p >= pairs) return;
     const int cap = P.plan.kp_cap;
-    const int nq = min(P.buf.nkp[p], cap), nt = min(P.buf.nkp[p + 1], cap);
+    const int nq = O.nq_fix >= 0 ? O.nq_fix : min(P.buf.nkp[p], cap);
+    const int nt = O.nt_fix >= 0 ? O.nt_fix : min(P.buf.nkp[p + 1], cap);
     const int qbase = qb * kMQB;
     if (qbase >= nq) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const v4i* XQ = reinterpret_cast<const v4i*>(P.buf.desc_x + (int64_t)p * cap * 256);
-    const v4i* XT = reinterpret_cast<const v4i*>(P.buf.desc_x + (int64_t)(p + 1) * cap * 256);
+    const uint4* XQ = reinterpret_cast<const uint4*>(O.q0 + p * O.stride);
+    const uint2* XT = reinterpret_cast<const uint2*>(O.t0 + p * O.stride);
     int32_t* fwd = P.buf.nn + (int64_t)p * cap;
     int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
     const int qs = qbase + wid * 64;  // this wave's first query
@@ -107,8 +130,12 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
         const int q = qs + 32 * s2 + r;
+        const uint4 w0 = q < nq ? XQ[2 * (int64_t)q] : make_uint4(0, 0, 0, 0);
+        const uint4 w1 = q < nq ? XQ[2 * (int64_t)q + 1] : make_uint4(0, 0, 0, 0);
+        const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) A[s2][ks] = q < nq ? scale_q(XQ[(int64_t)q * 16 + 2 * ks + h]) : (v4i){0, 0, 0, 0};
+        for (int ks = 0; ks < 8; ++ks)  // chunk 2 ks + h = half h of word ks; a zero fragment past nq
+            A[s2][ks] = q < nq ? expand16(wd[ks] >> (16 * h), kExpQ) : (v4i){0, 0, 0, 0};
 #pragma unroll
         for (int g = 0; g < 16; ++g) best[s2][g] = 0x7FFFFFFF;
     }
@@ -117,19 +144,17 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
     const bool full = qs + 64 <= nq;
     const int nst_all = (nt + kMStage - 1) / kMStage;
     const int st0 = (int)((int64_t)nst_all * ts / tsplit), nst = (int)((int64_t)nst_all * (ts + 1) / tsplit);
-    v4i v[kMStage * 16 / 256];
-    auto load_stage = [&](int st) {  // 4 chunks per thread (clamped index; zeroed past nt when stored)
-#pragma unroll
-        for (int it = 0; it < kMStage * 16 / 256; ++it) {
-            const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
-            v[it] = XT[(int64_t)min(st * kMStage + tr, nt - 1) * 16 + c];
-        }
-    };
+    // a stage: 64 trains x 32 bytes, 8 bytes (chunks 4 qd .. 4 qd + 3) per thread
+    const int tr = threadIdx.x >> 2, qd = threadIdx.x & 3;
+    uint2 v;
+    auto load_stage = [&](int st) { v = XT[(int64_t)min(st * kMStage + tr, nt - 1) * 4 + qd]; };  // clamped
     auto store_stage = [&](int st, int b) {
+        const bool in = st * kMStage + tr < nt;  // zero operands past nt
 #pragma unroll
-        for (int it = 0; it < kMStage * 16 / 256; ++it) {
-            const int i = threadIdx.x + 256 * it, tr = i >> 4, c = i & 15;
-            bt[b][tr * 16 + (c ^ (tr & 15))] = st * kMStage + tr < nt ? scale_t(v[it]) : (v4i){0, 0, 0, 0};
+        for (int c = 0; c < 4; ++c) {
+            const int ch = 4 * qd + c;
+            bt[b][tr * 16 + (ch ^ (tr & 15))] =
+                in ? expand16((c < 2 ? v.x : v.y) >> (16 * (c & 1)), kExpT) : (v4i){0, 0, 0, 0};
         }
         if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;
     };
@@ -166,33 +191,6 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, int pairs,
                 }
             }
         }
-}
-
-// Per-call operands: packed 32-byte descriptors (rows of q, then rows of t) to
-// the +-1 bytes nn_mfma_kernel reads (byte j of a row = bit j%8 of packed byte
-// j/8: any bijection works, both sides use the same), and the pair's counts.
-__global__ __launch_bounds__(256) void expand_desc_kernel(const uint8_t* __restrict__ q, int nq,
-                                                          const uint8_t* __restrict__ t, int nt, int cap,
-                                                          int8_t* __restrict__ x, int32_t* __restrict__ nkp) {
-    const int i = blockIdx.x * 256 + threadIdx.x;  // (row, 16-byte chunk)
-    if (i == 0) {
-        nkp[0] = nq;
-        nkp[1] = nt;
-    }
-    const int row = i >> 4, c = i & 15;
-    if (row >= nq + nt) return;
-    const uint8_t* src = row < nq ? q + (int64_t)row * 32 : t + (int64_t)(row - nq) * 32;
-    const int slot = row < nq ? row : cap + (row - nq);
-    const uint32_t bits = (uint32_t)src[2 * c] | ((uint32_t)src[2 * c + 1] << 8);
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v |= ((bits >> (4 * k + j)) & 1u ? 0x01u : 0xFFu) << (8 * j);
-        w[k] = v;
-    }
-    reinterpret_cast<uint4*>(x + (int64_t)slot * 256)[c] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 constexpr int kXNT = 1024;
@@ -367,7 +365,8 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
     if (e != hipSuccess) return e;
     const int pairs = P.nframes - 1, nqb = (cap + kMQB - 1) / kMQB;
     const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
-    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, pairs, nqb, 1);
+    const NnOperands O{P.buf.desc, P.buf.desc + (int64_t)cap * 32, (int64_t)cap * 32, -1, -1};
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, O, pairs, nqb, 1);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();
@@ -377,37 +376,31 @@ namespace {
 int pair_cap(int nq, int nt) { return ((nq > nt ? nq : nt) + kMQB - 1) / kMQB * kMQB; }
 }  // namespace
 
-size_t match_pair_work_size(int nq, int nt) {
-    const size_t cap = (size_t)pair_cap(nq, nt);
-    return 256 + 2 * cap * 256 + 3 * cap * sizeof(int32_t);
-}
+size_t match_pair_work_size(int nq, int nt) { return 3 * (size_t)pair_cap(nq, nt) * sizeof(int32_t); }
 
 // One pair through the stream's matcher: a StreamParams whose two "frames" are
-// the query and train sets (nkp = {nq, nt}, desc_x slots 0 and 1, nn = fwd |
-// unused | bwd), so nn_mfma_kernel runs unchanged, with the train stages split
-// over tsplit workgroups per query block to fill more than nq / 256 CUs.
+// the query and train sets (counts passed as nq_fix / nt_fix, operands the
+// caller's packed descriptors, nn = fwd | unused | bwd), so nn_mfma_kernel
+// runs unchanged, with the train stages split over tsplit workgroups per query
+// block to fill more than nq / 256 CUs.
 hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int cross_check, void* d_work,
                              dvo_dmatch* d_out, int* d_m, hipStream_t s) {
     const int cap = pair_cap(nq, nt);
     StreamParams P{};
     P.plan.kp_cap = cap;
     P.nframes = 2;
-    uint8_t* w = static_cast<uint8_t*>(d_work);
-    P.buf.nkp = reinterpret_cast<int32_t*>(w);
-    P.buf.desc_x = reinterpret_cast<int8_t*>(w + 256);
-    P.buf.nn = reinterpret_cast<int32_t*>(w + 256 + 2 * (size_t)cap * 256);
+    P.buf.nn = static_cast<int32_t*>(d_work);
     int32_t* fwd = P.buf.nn;
     int32_t* bwd = P.buf.nn + 2 * (size_t)cap;
     hipError_t e = hipMemsetAsync(P.buf.nn, 0x7F, sizeof(int32_t) * 3 * (size_t)cap, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(expand_desc_kernel, dim3((unsigned)(((nq + nt) * 16 + 255) / 256)), dim3(256), 0, s, d_q, nq,
-                       d_t, nt, cap, P.buf.desc_x, P.buf.nkp);
     const int nqb = cap / kMQB;
     const int nst = (nt + kMStage - 1) / kMStage;
     int tsplit = 1;
     while (tsplit < 16 && nqb * tsplit * 2 <= 256 && nst >= tsplit * 4) tsplit *= 2;  // <= 256 workgroups, >= 2 stages each
     const int nwg = ((nqb * tsplit + 7) / 8) * 8;
-    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, 1, nqb, tsplit);
+    const NnOperands O{d_q, d_t, 0, nq, nt};
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, O, 1, nqb, tsplit);
     hipLaunchKernelGGL(crosscheck_pair_kernel, dim3(1), dim3(kXNT), 0, s, fwd, bwd, nq, nt, cross_check, d_out, d_m);
     return hipGetLastError();
 }

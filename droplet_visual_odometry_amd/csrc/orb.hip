@@ -600,11 +600,14 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 //   NMS      per corner: strict 3x3 maximum -> keep bit of its row;
 //   output   keeps per tile row in column order, (offset << 16 | count) per
 //            row; select_fast_kernel restores raster order across tiles.
-// Minimum resident waves per SIMD requested of the compiler (VGPR budget): with the corner list
-// compacted into the candidate slots a workgroup needs ~18.4 KB of LDS, so 8 workgroups (8 waves
-// per SIMD) fit a CU when the kernel stays within 64 VGPRs.
+// Minimum resident waves per SIMD requested of the compiler (VGPR budget).  With the corner list
+// compacted into the candidate slots a workgroup needs ~18.4 KB of LDS, so 8 workgroups would fit a
+// CU, but the kernel then spills (64 VGPRs + 64 B/lane scratch at 8, 72 + 32 B at 7).  Measured,
+// whole default bench (profiles/r03e_ab_fast_occupancy.txt): 4 / 5 -> 70.5 K frames/s, 6 -> 73.0 K
+// (79 VGPRs, no spill), 7 -> 69.1 K, 8 -> 67.3 K: the FAST stage gets faster with occupancy but
+// starves the blur / describe kernels the other stream runs beside it.
 #ifndef DVO_FAST_WAVES_PER_EU
-#define DVO_FAST_WAVES_PER_EU 8
+#define DVO_FAST_WAVES_PER_EU 6
 #endif
 constexpr int kFtLW = 144;                      // LDS row stride of the image and score planes
 constexpr int kFtRows = kBandRows + 8;          // staged image rows per tile: [r0-4, r0+kBandRows+4)
@@ -1625,12 +1628,6 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         unsigned long long words[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) words[q] = __ballot(t0[q] < t1[q]);
-        {  // bits 4*lane .. 4*lane+3 as +-1 bytes: (nibble * 0x204081) & 0x01010101 spreads bit j to byte j
-            const unsigned long long wq = lane < 16 ? words[0] : lane < 32 ? words[1] : lane < 48 ? words[2] : words[3];
-            const uint32_t nib = (uint32_t)(wq >> ((4 * lane) & 63)) & 0xFu;
-            const uint32_t b01 = (nib * 0x00204081u) & 0x01010101u;
-            reinterpret_cast<uint32_t*>(P.buf.desc_x + ((int64_t)f * P.plan.kp_cap + k) * 256)[lane] = ~(b01 * 0xFEu);
-        }
         if (lane < 4) {
             unsigned long long* d = reinterpret_cast<unsigned long long*>(P.buf.desc + ((int64_t)f * P.plan.kp_cap + k) * 32);
             d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
