@@ -40,6 +40,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
 VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
 PMC_TRAFFIC = "r02z_pmc_traffic.json"  # tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes of the kernels
+# FP64 vector peak: 78.6 TFLOP/s, AMD's MI355X data-sheet figure (MI355X_MICROARCH.md lists no f64 row).  It is
+# the wave64 f64 FMA issue rate: 16 lanes per cycle per SIMD (a wave64 f64 instruction per 4 cycles) x 2 FLOP x
+# 1024 SIMDs x 2.4 GHz.
+F64_PEAK_TFLOPS = 78.6
+PMC_F64 = "r03f_pmc_f64.json"  # tools/pmc_stall_f64.sh + tools/pmc_f64.py: f64 VALU instructions per kernel
 
 
 def parse():
@@ -217,7 +222,8 @@ def main():
                     "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
                     "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
                     "path_frac": round(value * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9
-                                       / HBM_PEAK_GBS, 8)}
+                                       / HBM_PEAK_GBS, 8),
+                    "ransac_f64": ransac_f64(per_call.get("ransac"), W, H, N, B)}
 
     cpu = None
     pose_check = None
@@ -409,6 +415,33 @@ def pmc_counts(kernel, W, H, N, B):
             "traffic_raw": round((k["fetch_bytes_raw"] + k["write_bytes_raw"]) * scale),
             "calibrated": bool(k.get("calibrated")), "widths": k.get("widths"),
             "valu_insts": k.get("SQ_INSTS_VALU", 0.0) * scale, "source": src}
+
+
+def ransac_f64(ms_per_launch, W, H, N, B):
+    """f64 issue fraction of the RANSAC kernel group (sampling, stage A, Durand-Kerner, stage C, score,
+    replay, finish): its f64 VALU FLOPs per launch (profiles/PMC_F64: SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64,
+    FMA = 2 FLOP, a wave64 instruction = 64 lanes; scaled per pair from the profiled batch) / the group's
+    HIP-event time on the library stream / the FP64 vector peak.  The event time includes the waits for the
+    other stream's kernels sharing the CUs, so this is the rate the stage achieves in the pipeline."""
+    if not ms_per_launch:
+        return None
+    path = os.path.join(ROOT, "profiles", PMC_F64)
+    try:
+        doc = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    c = doc.get("config", {})
+    if (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
+        return None
+    scale = B / c["batch"]
+    ks = {k: v for k, v in doc["kernels"].items() if k.startswith("ransac_")}
+    flops = sum(v["f64_flops_full_wave"] for v in ks.values()) * scale
+    insts = sum(v["f64_wave_insts"] for v in ks.values()) * scale
+    achieved = flops / (ms_per_launch * 1e-3) / 1e12
+    return {"bound": "f64 valu", "achieved": round(achieved, 3), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / F64_PEAK_TFLOPS, 5), "f64_wave_insts_per_launch": round(insts),
+            "f64_flops_per_launch": round(flops), "ms_per_launch": round(ms_per_launch, 4),
+            "kernels": sorted(ks), "source": f"profiles/{PMC_F64} (batch {c['batch']}, scaled per pair to {B})"}
 
 
 def dropin_rate(pool, corners, K, nfeatures, seconds, n_frames=48):

@@ -382,7 +382,6 @@ GeomArgs stream_geom(dvo_stream* s) {
     g.cnt = s->buf.rcnt;
     g.subsets = s->buf.subsets;
     g.rs = s->buf.rs;
-    g.gscr = s->buf.gscr;
     g.fprec = s->buf.fprec;
     g.dk_off = s->buf.dk_off;
     g.dk_ctl = s->buf.dk_ctl;
@@ -437,7 +436,6 @@ int stream_alloc(dvo_stream* s) {
     A(b.rcnt, (size_t)F * hc * 10);
     A(b.subsets, (size_t)F * hc * 5);
     A(b.rs, (size_t)F);
-    A(b.gscr, (size_t)F * ((hc + 63) / 64) * 200 * 64);
     A(b.fprec, (size_t)F * ((hc + 63) / 64) * 128 * 64);
     A(b.dk_off, (size_t)F + 1);
     A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
@@ -1345,7 +1343,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     if (!(prob > 0 && prob < 1)) return fail(ctx, DVO_EINVAL, "prob must be in (0, 1)");
     if (m < 5) return fail(ctx, DVO_EFEWPTS, "fewer than 5 correspondences");
     HIP_TRY(hipSetDevice(ctx->device));
-    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *dgs, *drec, *doff, *dctl, *dlist;
+    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *drec, *doff, *dctl, *dlist;
     int rc;
     const size_t hc = (size_t)(max_iters > 1 ? max_iters : 1);
     Staging st;
@@ -1357,7 +1355,6 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 9, 16, &dinfo)) || (rc = scratch(ctx, 10, (size_t)m, &dmask)) ||
         (rc = scratch(ctx, 16, hc * 4, &dnmod)) || (rc = scratch(ctx, 17, hc * 40, &dcnt)) ||
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
-        (rc = scratch(ctx, 20, ((hc + 63) / 64) * 200 * 64 * 8, &dgs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
         (rc = scratch(ctx, 23, 4 * (2 + kDkMaxPasses), &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
         (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
@@ -1379,7 +1376,6 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.cnt = (int32_t*)dcnt;
     g.subsets = (int32_t*)dsub;
     g.rs = (RansacState*)drs;
-    g.gscr = (double*)dgs;
     g.fprec = (double*)drec;
     g.dk_off = (int32_t*)doff;
     g.dk_ctl = (int32_t*)dctl;

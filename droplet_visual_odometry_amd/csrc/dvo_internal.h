@@ -129,7 +129,6 @@ struct Buffers {
     int32_t* rcnt;        // [F][hyp_cap][10]
     int32_t* subsets;     // [F][hyp_cap][5]
     RansacState* rs;      // [F]
-    double* gscr;         // [F][ceil(hyp_cap / 64)][200][64]
     double* fprec;        // [F][ceil(hyp_cap / 64)][128][64]
     int32_t* dk_off;      // [F + 1]
     int32_t* dk_ctl;      // [2 + kDkMaxPasses]
@@ -187,7 +186,6 @@ struct GeomArgs {
     int32_t* cnt;           // [pairs][hyp_cap][10] inlier counts
     int32_t* subsets;       // [pairs][hyp_cap][5] sampled point indices
     RansacState* rs;        // [pairs]
-    double* gscr;           // [pairs][ceil(hyp_cap / 64)][200][64] five-point scratch
     double* fprec;          // [pairs][ceil(hyp_cap / 64)][128][64] five-point records
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
     int32_t* dk_ctl;        // [2 + kDkMaxPasses] -, pass-0 items, parked after pass k

@@ -255,12 +255,11 @@ __device__ __forceinline__ void mul_ql(const double* q, const double* l, double*
 
 // Rows: the nine entries of 2 EE^T E - tr(EE^T) E (row-major), then det E;
 // columns 0..9 go to L (the matrix OpenCV inverts), 10..19 to G (its RHS).
-// Rows of the 10x20 coefficient matrix, L = columns 0..9 and G = 10..19, are
-// written to strided per-thread columns (element k at X[k * 64]): L to LDS, G
-// to global scratch.  The null-space basis EE (4 x 9) is read from LDS
-// (EL[(c * 9 + e) * 64] = EE[c][e]) so the row loops stay rolled; E E^T entries
-// are formed per row block i (the three diagonal ones first, for the trace);
-// recomputed entries are bit-identical.
+// Both are register arrays (the row loops are unrolled, so every index is a
+// constant): the 1.6 KB per hypothesis never leaves the CU.  The null-space
+// basis EE (4 x 9) is read from LDS (EL[(c * 9 + e) * 64] = EE[c][e]); E E^T
+// entries are formed per row block i (the three diagonal ones first, for the
+// trace); recomputed entries are bit-identical.
 __device__ __forceinline__ void ee_entry(const double* EL, int e, double (&o)[4]) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) o[c] = EL[(c * 9 + e) * 64];
@@ -281,7 +280,7 @@ __device__ __forceinline__ void eet_entry(const double* EL, int i, int j, double
     }
 }
 
-__device__ __forceinline__ void coeff_matrix(const double* EL, double* L, double* G) {
+__device__ __forceinline__ void coeff_matrix(const double* EL, double (&L)[10][10], double (&G)[10][10]) {
     double tr[10];
     {
         double d0[10], d1[10], d2[10];
@@ -292,13 +291,13 @@ __device__ __forceinline__ void coeff_matrix(const double* EL, double* L, double
         for (int k = 0; k < 10; ++k) tr[k] = (d0[k] + d1[k]) + d2[k];
     }
     double row[20], c1[20], c2[20], t1[10], t2[10];
-#pragma unroll 1
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
         double Ei[3][10];
         eet_entry(EL, i, 0, Ei[0]);
         eet_entry(EL, i, 1, Ei[1]);
         eet_entry(EL, i, 2, Ei[2]);
-#pragma unroll 1
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
             double e0[4], e1[4], e2[4], eij[4];
             ee_entry(EL, 0 * 3 + j, e0);
@@ -315,9 +314,9 @@ __device__ __forceinline__ void coeff_matrix(const double* EL, double* L, double
             mul_ql(tr, eij, c1);
             const int r = i * 3 + j;
 #pragma unroll
-            for (int k = 0; k < 10; ++k) L[(r * 10 + k) * 64] = 2.0 * row[k] - c1[k];
+            for (int k = 0; k < 10; ++k) L[r][k] = 2.0 * row[k] - c1[k];
 #pragma unroll
-            for (int k = 0; k < 10; ++k) G[(r * 10 + k) * 64] = 2.0 * row[10 + k] - c1[10 + k];
+            for (int k = 0; k < 10; ++k) G[r][k] = 2.0 * row[10 + k] - c1[10 + k];
         }
     }
     double ea[4], eb[4];
@@ -341,9 +340,9 @@ __device__ __forceinline__ void coeff_matrix(const double* EL, double* L, double
     ee_entry(EL, 2, ea);
     mul_ql(t1, ea, c2);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) L[(90 + k) * 64] = (row[k] - c1[k]) + c2[k];
+    for (int k = 0; k < 10; ++k) L[9][k] = (row[k] - c1[k]) + c2[k];
 #pragma unroll
-    for (int k = 0; k < 10; ++k) G[(90 + k) * 64] = (row[10 + k] - c1[10 + k]) + c2[10 + k];
+    for (int k = 0; k < 10; ++k) G[9][k] = (row[10 + k] - c1[10 + k]) + c2[10 + k];
 }
 
 // LUImpl<double>(A, 10, b, 10, DBL_EPSILON*100) (matrix_decomp.cpp), split so
@@ -391,13 +390,13 @@ __device__ __forceinline__ bool lu10_factor(double (&A)[10][10], int (&piv)[10])
     return true;
 }
 
-// Gin: right-hand side (strided column, element k at Gin[k * 64]); solution
-// rows 4..9 go to X with the same layout.
-__device__ __forceinline__ void lu10_solve_cols(const double (&A)[10][10], const int (&piv)[10], const double* Gin, double* X) {
+// G: the right-hand side; solution rows 4..9 replace its rows 4..9.
+__device__ __forceinline__ void lu10_solve_cols(const double (&A)[10][10], const int (&piv)[10], double (&G)[10][10]) {
+#pragma unroll
     for (int c = 0; c < 10; c++) {
         double x[10];
 #pragma unroll
-        for (int r = 0; r < 10; r++) x[r] = Gin[(r * 10 + c) * 64];
+        for (int r = 0; r < 10; r++) x[r] = G[r][c];
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             const int k = piv[i];
@@ -419,7 +418,7 @@ __device__ __forceinline__ void lu10_solve_cols(const double (&A)[10][10], const
             x[i] = sacc / A[i][i];
         }
 #pragma unroll
-        for (int r = 4; r < 10; r++) X[(r * 10 + c) * 64] = x[r];
+        for (int r = 4; r < 10; r++) G[r][c] = x[r];
     }
 }
 
@@ -713,11 +712,11 @@ constexpr int kRecC = 0, kRecB = 11, kRecEE = 50, kRecRoots = 86, kRecNr = 106, 
 constexpr int kRecDoubles = 128;
 
 // Stage A: Q -> null space (JacobiSVD) -> 10x20 coefficient matrix -> LU solve
-// -> b -> degree-10 polynomial.  EL: this thread's LDS column of 36 doubles;
-// Gg: its global scratch column of 200 doubles ([0, 100) L, [100, 200) G,
-// overwritten in place by the solution rows 4..9).
-__device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, double* Gg, double* R) {
-    double* const G = Gg + 100 * 64;
+// -> b -> degree-10 polynomial.  EL: this thread's LDS column of 36 doubles.
+// The coefficient matrix and the solve stay in registers (L and G: 400 VGPRs
+// at the peak, one wave per SIMD as before; round 2 kept them in a 1.6 KB
+// global scratch column per hypothesis).
+__device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, double* R) {
     double At[9][9], W[5], Vt[5][5];
 #pragma unroll
     for (int i = 0; i < 9; ++i)
@@ -748,38 +747,36 @@ __device__ __forceinline__ void fp_stage_a(const double (&q)[5][4], double* EL, 
     double b[3 * 13];
     {
         // A = A.colRange(0,10).inv() * A.colRange(10,20) == solve(A1, A2, DECOMP_LU)
-        double L[10][10];
+        double L[10][10], G[10][10];
         int piv[10];
-        coeff_matrix(EL, Gg, G);
-#pragma unroll
-        for (int r = 0; r < 10; ++r)
-#pragma unroll
-            for (int k = 0; k < 10; ++k) L[r][k] = Gg[(r * 10 + k) * 64];
+        coeff_matrix(EL, L, G);
         if (lu10_factor(L, piv)) {
-            lu10_solve_cols(L, piv, G, G);
+            lu10_solve_cols(L, piv, G);
         } else {
 #pragma unroll
-            for (int k = 40; k < 100; ++k) G[k * 64] = 0;
+            for (int r = 4; r < 10; ++r)
+#pragma unroll
+                for (int k = 0; k < 10; ++k) G[r][k] = 0;
         }
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const double* a1 = G + (i * 2 + 4) * 10 * 64;
-            const double* a2 = G + (i * 2 + 5) * 10 * 64;
+            const double* a1 = G[i * 2 + 4];
+            const double* a2 = G[i * 2 + 5];
             double row1[13], row2[13];
 #pragma unroll
             for (int k = 0; k < 13; ++k) row1[k] = row2[k] = 0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row1[1 + k] = (a1[k * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row1[1 + k] = (a1[k] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row1[5 + k] = (a1[(3 + k) * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row1[5 + k] = (a1[3 + k] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) row1[9 + k] = (a1[(6 + k) * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 4; ++k) row1[9 + k] = (a1[6 + k] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row2[0 + k] = (a2[k * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row2[0 + k] = (a2[k] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) row2[4 + k] = (a2[(3 + k) * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 3; ++k) row2[4 + k] = (a2[3 + k] + 0.0) + 0.0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) row2[8 + k] = (a2[(6 + k) * 64] + 0.0) + 0.0;
+            for (int k = 0; k < 4; ++k) row2[8 + k] = (a2[6 + k] + 0.0) + 0.0;
 #pragma unroll
             for (int k = 0; k < 13; ++k) b[i * 13 + k] = row1[k] - row2[k];
         }
@@ -917,8 +914,8 @@ __device__ __forceinline__ void dk_store(double* R, Cx (&roots)[10]) {
 }
 
 // All three stages in one thread (test hook).  R: a 128-double record column.
-__device__ __forceinline__ int five_point(const double (&q)[5][4], double* models, double* EL, double* Gg, double* R) {
-    fp_stage_a(q, EL, Gg, R);
+__device__ __forceinline__ int five_point(const double (&q)[5][4], double* models, double* EL, double* R) {
+    fp_stage_a(q, EL, R);
     if (R[kRecGeneric * 64] == 0.0) {
         double c[11];
         Cx roots[10];
@@ -1254,8 +1251,7 @@ __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[i][k] = src[k];
     }
-    double* gg = g.gscr + ((int64_t)p * gridDim.x + blockIdx.x) * 200 * kSolveNT + threadIdx.x;
-    fp_stage_a(q, lds_g + threadIdx.x, gg, hyp_record(g, p, h));
+    fp_stage_a(q, lds_g + threadIdx.x, hyp_record(g, p, h));
 }
 
 // Durand-Kerner for every polynomial of the round, in passes that shrink the
@@ -2200,7 +2196,6 @@ __global__ void test_update_num_iters_kernel(double p, const double* ep, int n, 
     if (i < n) out[i] = ransac_update_num_iters(p, ep[i], mp, mi);
 }
 
-__device__ double g_test_gscr[200 * 64];
 __device__ double g_test_rec[kRecDoubles * 64];
 __global__ __launch_bounds__(64) void test_five_point_kernel(const double* qin, double* models, int* n) {
     __shared__ double lds_g[36 * 64];
@@ -2208,7 +2203,7 @@ __global__ __launch_bounds__(64) void test_five_point_kernel(const double* qin, 
     double q[5][4];
     for (int i = 0; i < 5; ++i)
         for (int k = 0; k < 4; ++k) q[i][k] = qin[i * 4 + k];
-    *n = five_point(q, models, lds_g, g_test_gscr, g_test_rec);
+    *n = five_point(q, models, lds_g, g_test_rec);
 }
 
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s) {

@@ -1,0 +1,38 @@
+"""Per-launch f64 VALU instruction counts of every kernel from the f64 PMC pass
+(tools/pmc_stall_f64.sh: SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 over a short
+one-stream bench, `launches` batch launches of `batch` new frames), as the JSON
+bench.py prices its RANSAC f64-issue fraction from.
+
+usage: python tools/pmc_f64.py <pmc_f64.csv> <out.json> [batch=512] [launches=2] [width height nfeatures]"""
+import csv
+import json
+import sys
+
+F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")
+
+
+def main(src, dst, batch=512, launches=2, width=1280, height=720, nfeatures=2000):
+    batch, launches = int(batch), int(launches)
+    kernels = {}
+    for r in csv.DictReader(open(src)):
+        d = int(r["dispatches"])
+        per = d / launches  # dispatches per batch launch; the CSV holds means per dispatch
+        k = {c.replace("SQ_INSTS_VALU_", "").lower(): float(r.get(c) or 0.0) * per for c in F64}
+        k["valu"] = float(r.get("SQ_INSTS_VALU") or 0.0) * per
+        k["waves"] = float(r.get("SQ_WAVES") or 0.0) * per
+        k["dispatches_per_launch"] = per
+        # wave64 f64 FLOPs if every lane were active: FMA = 2, others 1
+        k["f64_wave_insts"] = sum(k[c] for c in ("fma_f64", "mul_f64", "add_f64", "trans_f64"))
+        k["f64_flops_full_wave"] = 64.0 * (2 * k["fma_f64"] + k["mul_f64"] + k["add_f64"] + k["trans_f64"])
+        kernels[r["kernel"]] = k
+    doc = {"config": {"width": int(width), "height": int(height), "nfeatures": int(nfeatures), "batch": batch,
+                      "launches": launches},
+           "source": "rocprofv3 --pmc SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 SQ_INSTS_VALU SQ_WAVES (tools/pmc_stall_f64.sh)",
+           "kernels": kernels}
+    json.dump(doc, open(dst, "w"), indent=1)
+    for n, k in sorted(kernels.items(), key=lambda x: -x[1]["f64_wave_insts"])[:12]:
+        print(f"{n:40s} f64 wave-insts/launch {k['f64_wave_insts']:.4g}  valu {k['valu']:.4g}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
