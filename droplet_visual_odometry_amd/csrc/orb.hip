@@ -585,9 +585,11 @@ __device__ __forceinline__ uint32_t byte_at(uint32_t lo, uint32_t hi, int k) {  
 // NMS neighbourhood, score rows [r0-1, r1] x score columns [xs-1, xs+125): the
 // first tile computes all kBandRows+2 score rows, later tiles the kBandRows new ones and carry
 // the two above (and the corners of the last one, an output row of the next
-// tile, in a small list).  Per tile, phases separated by workgroup barriers;
-// the candidate lists are per-wave LDS segments that the next phase reads as
-// one concatenated list in full 64-lane rounds:
+// tile, in a small list).  Per tile, each wave runs compass -> segment test ->
+// score on its own rows with its own LDS list segment (no workgroup barrier
+// in between: at ~6% candidates a wave's list is about one 64-lane round, as
+// the concatenated list's share per wave was), then workgroup barriers
+// separate NMS (which reads neighbours' scores) and the output:
 //   compass  every pixel: a run of 9 on the 16-circle contains two adjacent
 //            compass pixels (0,4 / 4,8 / 8,12 / 12,0) that are both brighter
 //            or both darker: min(max(c0,c8), max(c4,c12)) > v+t, or the dual;
@@ -651,23 +653,6 @@ template <int kSeg>
 __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int e) {
     return list[seg_index<kSeg>(cnt, e)];
 }
-// The segment test reads the concatenated candidate list in rounds of kFastNT entries, wave w
-// taking entries [r kFastNT + 64 w, + 64) of round r, and compacts its corners in place: its
-// j-th corner overwrites its own j-th read entry (j < the entries it has read, so the slot is
-// consumed and no other wave reads it).  Concatenated corner e (corner counts cc[0..3]) is the
-// candidate entry returned here.
-__device__ __forceinline__ int corner_entry(const int* cc, int e, int nt) {
-    int w = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const bool past = e >= cc[k];
-        e -= past ? cc[k] : 0;
-        w += past ? 1 : 0;
-        if (!past) break;
-    }
-    return (e >> 6) * nt + 64 * w + (e & 63);
-}
-
 __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_kernel(StreamParams P, int nseg) {
     // nseg > 1 (batches of a few frames): a strip's tiles are walked by nseg workgroups,
     // segment k from tile k * ceil(nbands / nseg), each starting like tile 0 (2 more score rows)
@@ -692,10 +677,10 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
     __shared__ __attribute__((aligned(16))) uint8_t img[kFtRows * kFtLW];            // rows [r0-4, r0+kBandRows+4)
     __shared__ __attribute__((aligned(16))) uint8_t sc[(kBandRows + 2) * kFtLW];     // rows [r0-1, r0+kBandRows+1)
     // + 64 slots per wave that lanes without an entry store to (branch-free appends: no exec-mask SALU);
-    // the corners are compacted into the consumed candidate slots (corner_entry)
+    // a wave's corners are compacted into its consumed candidate slots
     __shared__ uint16_t cand[4 * kFtSegCand + 256];
     __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
-    __shared__ int ncand[4], ncorner[4], ncarry[2];
+    __shared__ int ncorner[4], ncarry[2];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
     __shared__ int row_off[4][kBandRows];
     const int lane = threadIdx.x & 63;
@@ -771,12 +756,15 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
                 pf[k] = q < kFtNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[k], bx + ynew * sp, 0) : 0u;
             }
         }
-        // ---- compass, four score pixels per lane: lane -> LDS word 1 + (lane & 31) of score row
-        // sr_lo + 2 (wid + 4 t) + (lane >> 5), t = 0, 1, ...
+        // ---- compass, segment test and score, each wave on its own rows, no workgroup barrier in
+        // between: the window is in LDS, a wave's candidates and corners are its own list segment and
+        // its scores land on its own score pixels.  Four score pixels per lane: lane -> LDS word
+        // 1 + (lane & 31) of score row sr_lo + 2 (wid + 4 t) + (lane >> 5), t = 0, 1, ...
         const int nsr = nrows + 2;
         const int sr_lo = b == b_begin ? 0 : 2;
+        const int seg_off = wid * kFtSegCand, spare_i = 4 * kFtSegCand + wid * 64 + lane;
+        int ncw = 0;  // this wave's corners (wave-uniform), compacted to cand[seg_off, seg_off + ncw)
         {
-            const int seg_off = wid * kFtSegCand, spare_i = 4 * kFtSegCand + wid * 64 + lane;
             int n = 0;  // wave-uniform
             for (int sr = sr_lo + 2 * wid + (lane >> 5); __builtin_amdgcn_readfirstlane(sr - (lane >> 5)) < nsr;
                  sr += 8) {
@@ -806,23 +794,17 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
                     n += __popcll(bal);
                 }
             }
-            if (lane == 0) ncand[wid] = n;
-        }
-        __syncthreads();
-        // ---- segment test over the concatenated candidates, corners compacted in place (corner_entry)
-        int cnt[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cnt[k] = ncand[k];
-        {
-            const int total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
-            const int spare = 4 * kFtSegCand + wid * 64 + lane;
-            int n = 0;
-            for (int e0 = wid * 64; e0 < total; e0 += kFastNT) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // segment test over the wave's candidates in 64-lane rounds; its j-th corner overwrites its
+            // j-th read entry (already consumed: j <= the entries read so far)
+            for (int e0 = 0; e0 < n; e0 += 64) {
                 const int e = e0 + lane;
                 bool is_corner = false;
                 int a = 0;
-                if (e < total) {
-                    a = seg_at<kFtSegCand>(cand, cnt, e);
+                if (e < n) {
+                    a = cand[seg_off + e];
                     const uint8_t* p = img + a;
                     const int v = p[0];
                     const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
@@ -836,12 +818,18 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
                     is_corner = has_run9(br) || has_run9(dk);
                 }
                 const unsigned long long bal = __ballot(is_corner);
-                const int j = n + (int)lane_prefix(bal);
-                cand[is_corner ? seg_index<kFtSegCand>(cnt, (j >> 6) * kFastNT + 64 * wid + (j & 63)) : spare] =
-                    (uint16_t)a;
-                n += __popcll(bal);
+                cand[is_corner ? seg_off + ncw + (int)lane_prefix(bal) : spare_i] = (uint16_t)a;
+                ncw += __popcll(bal);
             }
-            if (lane == 0) ncorner[wid] = n;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // scores of the wave's corners into the score plane
+            for (int e = lane; e < ncw; e += 64) {
+                const int a = cand[seg_off + e];
+                sc[a - 3 * kFtLW] = (uint8_t)fast_score16_pk(img + a, kFtLW, thr);
+            }
+            if (lane == 0) ncorner[wid] = ncw;
         }
         __syncthreads();
         int cnt2[4];
@@ -849,18 +837,12 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
         for (int k = 0; k < 4; ++k) cnt2[k] = ncorner[k];
         const int ncorners = cnt2[0] + cnt2[1] + cnt2[2] + cnt2[3];
         const int nc = ncarry[par];
-        // ---- scores of the new corners into the score plane
-        for (int e = threadIdx.x; e < ncorners; e += kFastNT) {
-            const int a = seg_at<kFtSegCand>(cand, cnt, corner_entry(cnt2, e, kFastNT));
-            sc[a - 3 * kFtLW] = (uint8_t)fast_score16_pk(img + a, kFtLW, thr);
-        }
-        __syncthreads();
         // score rows kBandRows, kBandRows+1 for the next tile (final now)
         if (threadIdx.x < 2 * kFtWords) screg = reinterpret_cast<const uint32_t*>(sc)[kBandRows * kFtWords + threadIdx.x];
         // ---- strict 3x3 NMS of the carried and new corners; keeps lie in rows [r0, r1), columns [xs, xe).
         // New corners of score row kBandRows+1 (row r0 + kBandRows) are the next tile's row-1 corners.
         for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
-            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCand>(cand, cnt, corner_entry(cnt2, e - nc, kFastNT))) -
+            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCand>(cand, cnt2, e - nc)) -
                           3 * kFtLW;  // score-plane address
             const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
             if (sr == kBandRows + 1) {
@@ -905,8 +887,7 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         for (int e = threadIdx.x; e < nc + ncorners; e += kFastNT) {
-            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCand>(cand, cnt, corner_entry(cnt2, e - nc, kFastNT))) -
-                          3 * kFtLW;
+            const int a = (e < nc ? (int)carry[par][e] : seg_at<kFtSegCand>(cand, cnt2, e - nc)) - 3 * kFtLW;
             const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
             if (sr < 1 || sr > nrows || x < xs || x >= xe) continue;
             const int i_col = x - (xs - 1), wq = i_col >> 5;
