@@ -1015,6 +1015,15 @@ __global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
 // [0, min(64, niters)) and round 2 everything left, [64, niters)
 // (kRansacBounds): the result is the sequential loop's, bit for bit.
 constexpr int kSolveNT = 64;
+// Wave issue priority of the RANSAC solver kernels (s_setprio, 0..3).  The other stream's ORB
+// kernels share the SIMDs with these long, latency-bound waves; a higher priority lets a solver
+// wave issue first whenever it is ready, and the throughput-bound ORB waves take the rest.
+#ifndef DVO_RANSAC_PRIO
+#define DVO_RANSAC_PRIO 0
+#endif
+__device__ __forceinline__ void dk_priority() {
+    if constexpr (DVO_RANSAC_PRIO > 0) __builtin_amdgcn_s_setprio(DVO_RANSAC_PRIO);
+}
 #ifndef DVO_SCORE_CHUNK
 #define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
 #endif
@@ -1235,6 +1244,7 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
 
 // Stage A of every hypothesis of the round (one thread each).
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
+    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
@@ -1282,6 +1292,7 @@ constexpr int kDkPasses = DVO_DK_B0 == 0 ? 1 : DVO_DK_B1 == 0 ? 2 : DVO_DK_B2 ==
 constexpr int kRecSnap = 108;                     // parked: Brent snapshot (20 doubles)
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
+    dk_priority();
     // pass 0: items [0, dk_ctl[1]) of the round's work list; pass k > 0: dk_list[k - 1][0, dk_ctl[1 + k])
     const int total = g.dk_ctl[1 + pass];
     if ((int)blockIdx.x * kDkNT >= total) return;
@@ -1469,6 +1480,7 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
 
 // Stage C of every hypothesis of the round: models and their count.
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
+    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
@@ -1550,6 +1562,7 @@ __global__ __launch_bounds__(64) void ransac_stage_c_row_kernel(GeomArgs g) {
 // so that its few blocks spread over more CUs (fewer models per wave in sequence).
 template <int HYPS>
 __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
+    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int hb = S.h0 + blockIdx.x * HYPS;

@@ -617,6 +617,7 @@ static_assert(kFastTW == 124 && (kBorder - 7) % 4 == 0, "FAST tiles: score colum
 // per-wave list capacities: compass, row pairs wid, wid+4, .. of 64 lanes x 4 px; segment test, the
 // concatenated candidates of the tile (<= (kBandRows + 2) x 126) in 64-lane rounds of the 4 waves
 constexpr int kFtSegCand = ((kBandRows + 3) / 2 + 3) / 4 * 256;
+constexpr int kFtWordCand = kFtSegCand / 4;  // compass word entries per wave (64 lanes x iterations)
 constexpr int kFtWords = kFtLW / 4;             // words per staged row
 constexpr int kFtNewW = kBandRows * kFtWords;   // words loaded per tile (rows r0+4 .. r0+kBandRows+4)
 constexpr int kFtPf = (kFtNewW + kFastNT - 1) / kFastNT;
@@ -679,6 +680,7 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
     // + 64 slots per wave that lanes without an entry store to (branch-free appends: no exec-mask SALU);
     // a wave's corners are compacted into its consumed candidate slots
     __shared__ uint16_t cand[4 * kFtSegCand + 256];
+    __shared__ uint16_t wlist[4 * kFtWordCand + 256];  // per-wave word entries of the compass (+ spare slots)
     __shared__ uint16_t carry[2][kFtCarryList];  // corners of score row r0+16, as next-tile addresses
     __shared__ int ncorner[4], ncarry[2];
     __shared__ uint32_t keep[kBandRows][4];  // bit i <-> score column xs - 1 + i
@@ -765,7 +767,8 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
         const int seg_off = wid * kFtSegCand, spare_i = 4 * kFtSegCand + wid * 64 + lane;
         int ncw = 0;  // this wave's corners (wave-uniform), compacted to cand[seg_off, seg_off + ncw)
         {
-            int n = 0;  // wave-uniform
+            int n = 0, nw = 0;  // wave-uniform: pixel candidates, words with one
+            const int wl_off = wid * kFtWordCand, wl_spare = 4 * kFtWordCand + wid * 64 + lane;
             for (int sr = sr_lo + 2 * wid + (lane >> 5); __builtin_amdgcn_readfirstlane(sr - (lane >> 5)) < nsr;
                  sr += 8) {
                 const int base = (sr + 3) * kFtLW + c_col;  // centre-row byte address of the word
@@ -783,16 +786,38 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
                                                   as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C030C01)),
                                                   as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C060C04)),
                                                   as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C040C02)), thr2);
-                // byte k of pm nonzero <=> pixel k passes and is a score pixel of this tile
+                // byte k of pm nonzero <=> pixel k passes and is a score pixel of this tile; bit k of
+                // msk the same (bit 7 of each byte <- byte != 0, then the 4 bits gathered by one multiply)
                 const uint32_t pm = (r0p | (r1p << 8)) & (sr < nsr ? c_vm : 0u);
+                const uint32_t nzb = ((((pm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | pm) >> 7) & 0x01010101u;
+                const uint32_t msk = (nzb * 0x10204080u) >> 28;
+                // one entry per word with a passing pixel: (word index | mask << 12)
+                const bool any = msk != 0;
+                const unsigned long long bal = __ballot(any);
+                const int to = wl_off + nw + (int)lane_prefix(bal);
+                wlist[any ? to : wl_spare] = (uint16_t)((base >> 2) | (msk << 12));
+                nw += __popcll(bal);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // word entries -> pixel entries: a lane's c = popc(mask) pixels go to its prefix of c
+            // (from three ballots of c's bits) plus the rank of the pixel's bit in the mask
+            for (int e0 = 0; e0 < nw; e0 += 64) {
+                const int e = e0 + lane;
+                const uint32_t ent = e < nw ? (uint32_t)wlist[wl_off + e] : 0u;
+                const uint32_t msk = ent >> 12;
+                const int a0 = (int)(ent & 0xFFFu) << 2;
+                const uint32_t c = (uint32_t)__popc(msk);
+                const unsigned long long b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+                const int pre = n + (int)lane_prefix(b0) + 2 * (int)lane_prefix(b1) + 4 * (int)lane_prefix(b2);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const bool pass = ((pm >> (8 * k)) & 0xFF) != 0;
-                    const unsigned long long bal = __ballot(pass);
-                    const int to = seg_off + n + (int)lane_prefix(bal);
-                    cand[pass ? to : spare_i] = (uint16_t)(base + k);
-                    n += __popcll(bal);
+                    const bool on = (msk >> k) & 1u;
+                    const int to = seg_off + pre + __popc(msk & ((1u << k) - 1u));
+                    if (on) cand[to] = (uint16_t)(a0 + k);
                 }
+                n += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
