@@ -66,6 +66,9 @@ struct dvo_stream {
     int last_nframes = 0;
     bool last_has_pairs = false;  // the last call ran match + geometry
     const dvo_pair_record* last_rec = nullptr;  // the caller's records of that call (read by the pose tail)
+    const uint8_t* last_frames = nullptr;       // the frames of that call (get_pyramid recomputes blurred levels)
+    int64_t last_fstride = 0;
+    int last_pitch = 0;
     hipStream_t hs = nullptr;
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
@@ -510,6 +513,9 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
     HIP_TRY(launch_orb(P, s->hs, ev));
     s->last_nframes = n;
+    s->last_frames = d_frames;
+    s->last_fstride = fstride;
+    s->last_pitch = pitch;
     s->last_has_pairs = !detect_only && n >= 2;
     s->last_rec = d_rec;
     if (!s->last_has_pairs) return DVO_OK;
@@ -785,6 +791,12 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
     const LevelGeom& G = s->plan.L[level];
     if (cap < G.w * G.h) return fail(ctx, DVO_ECAP, "capacity too small");
     HIP_TRY(hipStreamSynchronize(s->hs));
+    if (blurred && describe_blurs()) {
+        // the detection path blurs only the descriptor windows (describe_kernel): the whole blurred
+        // pyramid is recomputed here from the last call's frames, which must still be alive
+        HIP_TRY(launch_blur(params_of(s, s->last_frames, s->last_nframes, s->last_fstride, s->last_pitch), s->hs));
+        HIP_TRY(hipStreamSynchronize(s->hs));
+    }
     if (blurred) {
         HIP_TRY(hipMemcpy2D(out, G.w, s->buf.blur + (size_t)frame * s->plan.blur_stride + G.blur_off, G.bpitch, G.w,
                             G.h, hipMemcpyDeviceToHost));

@@ -277,6 +277,10 @@ inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
     if (ev) hipEventRecord(ev[2 * stage + end], s);
 }
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nullptr);
+// GaussianBlur of every level into Buffers::blur.  On the detection path only when describe_kernel
+// reads a blurred pyramid (describe_blurs() false); otherwise for dvo_stream_get_pyramid(blurred).
+hipError_t launch_blur(const StreamParams& P, hipStream_t s);
+bool describe_blurs();
 hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev = nullptr);
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
                            hipEvent_t* ev = nullptr);

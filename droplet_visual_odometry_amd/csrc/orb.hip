@@ -6,14 +6,17 @@
 //
 // Stages (DESIGN.md §4 lists the roofline of each):
 //   resize_level_kernel   INTER_LINEAR_EXACT 8-bit fixed point, level l-1 -> l
-//   blur_kernel           GaussianBlur 7x7 sigma 2, 8-bit fixed-point separable
+//   blur_kernel           GaussianBlur 7x7 sigma 2, 8-bit fixed-point separable, of every level:
+//                         only for dvo_stream_get_pyramid(blurred) when describe_kernel
+//                         blurs its own windows (DVO_DESCRIBE_BLUR, the default)
 //   fast_strip_kernel     FAST-9/16 + strict 3x3 NMS + border cut + per-row
 //                         compaction, one column strip of one level per workgroup
 //   select_fast_kernel    KeyPointsFilter::retainBest(2n) by FAST score: exact
 //                         emulation of libstdc++ nth_element + partition
 //   harris_kernel         HarrisResponses(blockSize 7, k 0.04)
 //   select_harris_kernel  retainBest(n) by Harris response
-//   describe_kernel       ICAngles + pt scaling + rBRIEF-256, one wave per keypoint
+//   describe_kernel       ICAngles + pt scaling + GaussianBlur of the 39 x 44 sample window
+//                         + rBRIEF-256, one wave per keypoint
 #include "dvo_internal.h"
 
 #include <climits>
@@ -1452,12 +1455,84 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // blurred 39 x 44 window around it (word loads into LDS); the 512 rBRIEF
 // samples are then LDS reads.
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
+// keypoints per wave, the loads of all of them requested first.  Reading a blurred pyramid: 1 73.0 K,
+// 2 73.6 K, 4 72.3 K frames/s (profiles/r02z_ab_describe_dkw.txt); blurring the windows here
+// (DVO_DESCRIBE_BLUR, 16 raw rows per lane and keypoint): 1 74.8 K (51 VGPRs), 2 74.3 K (119 VGPRs),
+// against 73.2 K for the separate blur pass (profiles/r03o_ab_describe_blur.txt)
 #ifndef DVO_DKW
-#define DVO_DKW 2  // keypoints per wave, loads of all requested first: 1 73.0 K, 2 73.6 K, 4 72.3 K frames/s (profiles/r02z_ab_describe_dkw.txt)
+#define DVO_DKW 1
 #endif
 constexpr int kDKW = DVO_DKW;          // keypoints per wave
 constexpr int kDKB = 4 * kDKW;         // keypoints per workgroup
 constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padding) x 9 aligned words
+
+// DVO_DESCRIBE_BLUR: the GaussianBlur of the 39 x 44 window is computed here from
+// the raw level instead of being read from a blurred copy of the pyramid written
+// by blur_kernel (which then does not run on the detection path).  Lane
+// (s, wc) = (lane / 13, lane % 13), s < 4 (lanes 52..63 idle): raw word wc of the
+// window row span [a0 - 4, a0 + 48) (words 0 and 12 are the horizontal halo), 10
+// output rows 10 s .. 10 s + 9 of the patch from 16 raw rows, the vertical
+// 7-tap over a rolling window of u16 pairs and the horizontal taps from the
+// neighbouring lanes (wave_shr / wave_shl), with blur_wave's arithmetic and
+// rounding rule (half to even below w & ~3, half up in the w % 4 tail).
+// Keypoints lie >= 31 pixels from every border and the window reaches 22, so
+// no reflection is needed.
+#ifndef DVO_DESCRIBE_BLUR
+#define DVO_DESCRIBE_BLUR 1
+#endif
+constexpr int kDBRows = 10, kDBSeg = 4, kDBRaw = kDBRows + 6;  // output rows per lane segment, segments, raw rows
+
+__device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw], uint8_t* patch_slot, int s, int wc,
+                                                   bool he) {
+    const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
+    const uint32_t R = he ? 0x7FFFu : 0x8000u;
+    u16x2 lo[7], hi[7];
+#pragma unroll
+    for (int r = 0; r < kDBRaw; ++r) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            lo[k] = lo[k + 1];
+            hi[k] = hi[k + 1];
+        }
+        lo[6] = as_u16x2(__builtin_amdgcn_perm(0u, raw[r], 0x0C010C00u));  // (b0, b1)
+        hi[6] = as_u16x2(__builtin_amdgcn_perm(0u, raw[r], 0x0C030C02u));  // (b2, b3)
+        if (r < 6) continue;
+        const u16x2 a = k18 * (lo[0] + lo[6]) + k34 * (lo[1] + lo[5]) + k49 * (lo[2] + lo[4]) + k55 * lo[3];
+        const u16x2 b = k18 * (hi[0] + hi[6]) + k34 * (hi[1] + hi[5]) + k49 * (hi[2] + hi[4]) + k55 * hi[3];
+        const uint32_t A = __builtin_bit_cast(uint32_t, a), B = __builtin_bit_cast(uint32_t, b);
+        const u16x2 al = as_u16x2(dpp_from_left(A)), bl = as_u16x2(dpp_from_left(B));
+        const u16x2 ar = as_u16x2(dpp_from_right(A)), br = as_u16x2(dpp_from_right(B));
+        uint32_t s0 = __builtin_amdgcn_udot2(al, (u16x2){0, 18}, R, false);
+        s0 = __builtin_amdgcn_udot2(bl, (u16x2){34, 49}, s0, false);
+        s0 = __builtin_amdgcn_udot2(a, (u16x2){55, 49}, s0, false);
+        s0 = __builtin_amdgcn_udot2(b, (u16x2){34, 18}, s0, false);
+        uint32_t s1 = __builtin_amdgcn_udot2(bl, (u16x2){18, 34}, R, false);
+        s1 = __builtin_amdgcn_udot2(a, (u16x2){49, 55}, s1, false);
+        s1 = __builtin_amdgcn_udot2(b, (u16x2){49, 34}, s1, false);
+        s1 = __builtin_amdgcn_udot2(ar, (u16x2){18, 0}, s1, false);
+        uint32_t s2 = __builtin_amdgcn_udot2(bl, (u16x2){0, 18}, R, false);
+        s2 = __builtin_amdgcn_udot2(a, (u16x2){34, 49}, s2, false);
+        s2 = __builtin_amdgcn_udot2(b, (u16x2){55, 49}, s2, false);
+        s2 = __builtin_amdgcn_udot2(ar, (u16x2){34, 18}, s2, false);
+        uint32_t s3 = __builtin_amdgcn_udot2(a, (u16x2){18, 34}, R, false);
+        s3 = __builtin_amdgcn_udot2(b, (u16x2){49, 55}, s3, false);
+        s3 = __builtin_amdgcn_udot2(ar, (u16x2){49, 34}, s3, false);
+        s3 = __builtin_amdgcn_udot2(br, (u16x2){18, 0}, s3, false);
+        s0 += __builtin_amdgcn_ubfe(s0, 16, he);
+        s1 += __builtin_amdgcn_ubfe(s1, 16, he);
+        s2 += __builtin_amdgcn_ubfe(s2, 16, he);
+        s3 += __builtin_amdgcn_ubfe(s3, 16, he);
+        s0 = min(s0, 0xFFFFFFu);
+        s1 = min(s1, 0xFFFFFFu);
+        s2 = min(s2, 0xFFFFFFu);
+        s3 = min(s3, 0xFFFFFFu);
+        const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0C0C0602u),
+                                                    __builtin_amdgcn_perm(s1, s0, 0x0C0C0602u), 0x05040100u);
+        const int i = kDBRows * s + (r - 6);  // patch row
+        if (s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH)
+            reinterpret_cast<uint32_t*>(patch_slot + i * kDPW)[wc - 1] = word;
+    }
+}
 
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[kDKB][kDPH + 2][kDPW];  // + 2 padding rows
@@ -1522,7 +1597,12 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     // ---- phase 1: every keypoint of this wave requests both windows first (one load latency
     // covers the wave's kDKW keypoints), then each is staged in LDS and gets its IC angle
     constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
+#if DVO_DESCRIBE_BLUR
+    uint32_t ivs[kDKW][5], pvs[kDKW][kDBRaw];
+    const int db_s = lane / 13, db_wc = lane - 13 * db_s;  // lanes >= 52: segment 4 (loads in range, no store)
+#else
     uint32_t ivs[kDKW][5], pvs[kDKW][7];
+#endif
 #pragma unroll
     for (int kk = 0; kk < kDKW; ++kk) {  // slots past nk read the clamped last keypoint (unused)
         const int l = lv[kk];
@@ -1536,19 +1616,35 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         const int ai = (kx - 15) & ~3;
         const int step = level_pitch(P, l);
         const uint8_t* img = level_ptr(P, f, l) + (int64_t)(ky - 15) * step + ai;
-        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * G.bpitch + a0;
+#ifdef DVO_EXP_SKIP_BLUR  // timing experiment: sample the unblurred level (descriptors still discriminate)
+        const int bpitch = step;
+        const uint8_t* bl = level_ptr(P, f, l) + (int64_t)(cyb - kDPR) * bpitch + a0;
+#else
+        const int bpitch = G.bpitch;
+        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * bpitch + a0;
+#endif
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const int ec = min(64 * t + lane, kIW - 1);
             const int rc = ec / (kICW / 4), wc = ec - rc * (kICW / 4);
             ivs[kk][t] = *reinterpret_cast<const uint32_t*>(img + (int64_t)rc * step + 4 * wc);
         }
+#if DVO_DESCRIBE_BLUR
+        {  // raw rows cyb - 22 + 10 s .. + 15 of word db_wc of [a0 - 4, a0 + 48)
+            const int sr = min(db_s, kDBSeg - 1);
+            const uint8_t* rw = level_ptr(P, f, l) + (int64_t)(cyb - kDPR - 3 + kDBRows * sr) * step + a0 - 4 + 4 * db_wc;
+#pragma unroll
+            for (int t = 0; t < kDBRaw; ++t) pvs[kk][t] = *reinterpret_cast<const uint32_t*>(rw + (int64_t)t * step);
+            (void)bl;
+        }
+#else
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
             const int ec = min(64 * t + lane, kPW - 1);
             const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
-            pvs[kk][t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * G.bpitch + 4 * wc);
+            pvs[kk][t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * bpitch + 4 * wc);
         }
+#endif
     }
 #pragma unroll
     for (int kk = 0; kk < kDKW; ++kk) {
@@ -1568,8 +1664,13 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
+#if DVO_DESCRIBE_BLUR
+        describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc,
+                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w);
+#else
 #pragma unroll
         for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pvs[kk][t];
+#endif
         __builtin_amdgcn_wave_barrier();
         // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
         const uint8_t* col = &icw[wv][0][0] + (kx - ai) + u;
@@ -1650,6 +1751,13 @@ __global__ void test_retain_best_kernel(float* resp, uint32_t* payload, int32_t*
 
 }  // namespace
 
+hipError_t launch_blur(const StreamParams& P, hipStream_t s) {
+    hipLaunchKernelGGL(blur_kernel, dim3(P.plan.total_tiles * xcd_frames(P.nframes)), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+bool describe_blurs() { return DVO_DESCRIBE_BLUR != 0; }
+
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const Plan& pl = P.plan;
     const int F = P.nframes;
@@ -1673,7 +1781,9 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
+#if !defined(DVO_EXP_SKIP_BLUR) && !DVO_DESCRIBE_BLUR  // describe blurs its own windows (DVO_DESCRIBE_BLUR)
     hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
+#endif
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);

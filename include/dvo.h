@@ -282,7 +282,12 @@ int dvo_pose_chain(dvo_ctx* ctx, const double* d_T_rel, int n, double* d_T_carry
 int dvo_stream_set_profiling(dvo_stream* s, int enable);
 int dvo_stream_stage_times(dvo_stream* s, double* ms /* DVO_NSTAGES */, int* calls);
 
-/* Host copies of intermediate results of the last dvo_stream_process (tests). */
+/* Host copies of intermediate results of the last dvo_stream_process (tests).
+ * get_pyramid(blurred = 1): the detection path blurs only the 39 x 44 descriptor
+ * windows inside the describe kernel, so the whole GaussianBlur of the level is
+ * computed on this call from the last process's frames, which must still be
+ * alive (device frames passed to dvo_stream_process, or the stream's own upload
+ * slab). */
 int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t* desc, int cap, int* n);
 int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m);
 int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uint8_t* out, int cap);
