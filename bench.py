@@ -82,10 +82,10 @@ def stage_bytes(w, h, nfeatures, n_matches):
     n = nfeatures
     return {
         "pyramid": float(sum(px[l - 1] + px[l] for l in range(1, 8))),  # read l-1, write l
-        "blur": float(2 * sum(px)),                                    # read + write every level
+        "blur": 0.0,                                                   # no separate pass: describe blurs its windows
         "fast": float(sum(px)),                                        # read every level once
         "select_harris": float(8 * 2 * n + 81 * 2 * n),                 # keys + 9x9 Harris windows
-        "describe": float(n * (749 + 512 + 28 + 32)),                  # angle disc + pattern + kp + desc
+        "describe": float(n * (749 + 45 * 52 + 28 + 32)),              # angle disc + raw 45x52 window + kp + desc
         "match": float(2 * 2 * n * 32 + 16 * n_matches),               # both directions read both sets
         "ransac": float(32 * n_matches),                               # normalised correspondences
         "recover_pose": float(32 * n_matches + 256),
