@@ -18,12 +18,14 @@ namespace dvo {
 constexpr int kMaxLevels = 8;
 // OpenCV semantics of the ORB path (dvo_orb_params.opencv_semantics): 4.x or 3.2.
 constexpr int kOcv4 = DVO_OPENCV_4X, kOcv32 = DVO_OPENCV_32;
-// FAST tile height (output rows).  Two-stream bench, 1280x720: 16 rows 66.8-67.2 K
-// frames/s, 20: 67.7 K, 24: 68.2-69.1 K, 28: 65.7-66.1 K, 32: 67.1-67.9 K
-// (taller tiles: fewer barriers and carried rows per output row, more LDS per
-// workgroup; 24 rows = 6 workgroups per CU).
+// FAST tile height (output rows).  Two-stream bench, 1280x720, round 2 kernel: 16 rows
+// 66.8-67.2 K frames/s, 20: 67.7 K, 24: 68.2-69.1 K, 28: 65.7-66.1 K, 32: 67.1-67.9 K.  Round 3
+// (per-wave compass/segment/score, word candidate lists, no separate blur pass;
+// profiles/r03p_ab_fast_band_rows.txt, r03q_*): 20 73.7 K, 24 75.0 K, 28 75.9 K, 32 77.9 K
+// (26 KB of LDS, still 6 workgroups per CU), 40 77.8 K (5 per CU), 48 76.9 K, 64 75.7 K:
+// taller tiles cost fewer barriers and carried rows per output row.
 #ifndef DVO_BAND_ROWS
-#define DVO_BAND_ROWS 24
+#define DVO_BAND_ROWS 32
 #endif
 constexpr int kBandRows = DVO_BAND_ROWS;
 constexpr int kFastTW = 124;        // FAST tile width (output columns; score columns 126 = LDS words 1..32)
