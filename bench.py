@@ -434,7 +434,7 @@ def ransac_f64(ms_per_launch, W, H, N, B):
     if (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
         return None
     scale = B / c["batch"]
-    ks = {k: v for k, v in doc["kernels"].items() if k.startswith("ransac_")}
+    ks = {k: v for k, v in doc["kernels"].items() if "ransac_" in k}  # incl. "void ransac_score_kernel<16>"
     flops = sum(v["f64_flops_full_wave"] for v in ks.values()) * scale
     insts = sum(v["f64_wave_insts"] for v in ks.values()) * scale
     achieved = flops / (ms_per_launch * 1e-3) / 1e12
