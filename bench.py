@@ -438,8 +438,11 @@ def ransac_f64(ms_per_launch, W, H, N, B):
     flops = sum(v["f64_flops_full_wave"] for v in ks.values()) * scale
     insts = sum(v["f64_wave_insts"] for v in ks.values()) * scale
     achieved = flops / (ms_per_launch * 1e-3) / 1e12
+    # issue view: a wave64 f64 instruction holds a SIMD's f64 pipe 4 cycles (16 lanes per cycle)
+    issue = insts * 4 / (ms_per_launch * 1e-3 * 1024 * 2.4e9)
     return {"bound": "f64 valu", "achieved": round(achieved, 3), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / F64_PEAK_TFLOPS, 5), "f64_wave_insts_per_launch": round(insts),
+            "frac": round(achieved / F64_PEAK_TFLOPS, 5), "issue_frac": round(issue, 5),
+            "f64_wave_insts_per_launch": round(insts),
             "f64_flops_per_launch": round(flops), "ms_per_launch": round(ms_per_launch, 4),
             "kernels": sorted(ks), "source": f"profiles/{PMC_F64} (batch {c['batch']}, scaled per pair to {B})"}
 
