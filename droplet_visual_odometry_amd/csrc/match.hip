@@ -6,7 +6,7 @@
 // (v3:355, v3:358).
 //
 // nn_mfma_kernel: forward and backward nearest neighbours of a pair on the
-// matrix cores (int8 MFMA over descriptor bits expanded to +-64 bytes), for the batched stream
+// matrix cores (block-scaled fp4 MFMA over descriptor bits as +-1.0), for the batched stream
 // and, through a one-pair parameter block, for the per-call C-ABI.
 // crosscheck_*_kernel: mutual-NN filter, then a bitonic sort of the unique
 // keys (distance << 16 | queryIdx) in LDS, then the point gather.
@@ -22,15 +22,15 @@ namespace {
 // Forward + backward nearest neighbours of one stream pair on the matrix cores.
 // The operands are the packed 32-byte descriptors (P.buf.desc, as described;
 // the per-call path's caller buffers), expanded in registers on the way in:
-// every descriptor bit becomes a byte, +64 on the query side and -64 on the
-// train side when set (the opposite sign when clear), so the
-// v_mfma_i32_32x32x32_i8 accumulator is D = -4096 s where s = q.t = 256 -
-// 2 * Hamming(q, t), exact in int32.  Then key = 2^20 + D + index =
+// every descriptor bit becomes an operand element, +1 on the query side and
+// -1 on the train side when set (the opposite sign when clear), scaled so the
+// accumulator is D = -4096 s where s = q.t = 256 - 2 * Hamming(q, t), exact
+// (format below).  Then key = 2^20 + D + index =
 // Hamming * 8192 + index (index < 8192): one add per element and direction,
 // and the minimum key is OpenCV's nearest neighbour with its first-index tie
 // rule.  A wave owns 64 queries (two 32-row strips, A fragments resident in
 // VGPRs); the workgroup streams the trains through LDS 64 at a time (2 KB of
-// packed rows per stage, 16 KB expanded), double-buffered (the next stage's
+// packed rows per stage, 8 KB expanded), double-buffered (the next stage's
 // global loads are in flight during this stage's MFMAs; one barrier per
 // stage), 16-byte chunks XOR-swizzled by train so the b128 fragment reads are
 // conflict-free.  Forward keys fold into a per-register running minimum (the
@@ -41,47 +41,118 @@ namespace {
 // (blocks b and b + 8 share one) so the query blocks of a pair stream its
 // trains through one L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kMWaves = 4, kMQB = 64 * kMWaves, kMStage = 64;
-constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^22), < 0x7F7F7F7F
 constexpr int kKeyBase = 1 << 20;     // 256 * 4096
 
+// Operand format.  DVO_MATCH_FP4=1 (default): v_mfma_scale_f32_32x32x64_f8f6f4
+// on e2m1 (fp4) operands, +-1.0 per descriptor bit (a nibble each: 32 bits of
+// a descriptor word = one 16-byte chunk), the train side's block scale 2^12, so
+// the f32 accumulator is D = -4096 s exactly (integers < 2^21); keys are formed
+// in f32 (exact below 2^24) and compared as the bit patterns of non-negative
+// floats (ordered like the values).  Twice the i8 form's K per clock and half
+// its LDS bytes per train.  DVO_MATCH_FP4=0: the i8 form
+// (v_mfma_i32_32x32x32_i8, +-64 bytes, 16 chunks of 16 bits per train).
+#ifndef DVO_MATCH_FP4
+#define DVO_MATCH_FP4 1
+#endif
+#if DVO_MATCH_FP4
+constexpr int kMChunks = 8;   // 16-byte operand chunks per train
+constexpr int kMKs = 4;       // MFMAs per 32x32 block
+constexpr int kChunkBits = 32;
+typedef v16f acc_t;
+constexpr int kKeyNone = 0x7F000000;  // bits of ~1.7e38f: above every key, not a NaN
+// 32 descriptor bits to 32 e2m1 nibbles (a permutation of the bit order that A
+// and B share, so the dot product is unchanged): nibble-spread of byte k is
+// L | H << 4, L / H the byte's low / high nibble spread to bytes by
+// (n * 0x204081) & 0x01010101; bit 3 of a nibble is the e2m1 sign, so
+// base ^ (spread << 3) is 0x2 (+1.0) or 0xA (-1.0).  Query base 0xAA.. (set ->
+// +1), train base 0x22.. (set -> -1).
+__device__ __forceinline__ v4i expand_chunk(uint32_t bits, uint32_t base) {
+    v4i r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t L = (((bits >> (8 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        const uint32_t H = (((bits >> (8 * k + 4)) & 0xFu) * 0x00204081u) & 0x01010101u;
+        r[k] = (int)(base ^ (L << 3) ^ (H << 7));
+    }
+    return r;
+}
+constexpr uint32_t kExpQ = 0xAAAAAAAAu, kExpT = 0x22222222u;
+__device__ __forceinline__ acc_t mfma_chunk(v4i a, v4i b, acc_t c) {
+    const v8i A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    // cbsz = blgp = 4 (e2m1); E8M0 scales 127 (1.0) for A, 139 (2^12) for B
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, 0x7F7F7F7F, 0, 0x8B8B8B8B);
+}
+// key bits of accumulator element a plus the exact integer c (both as f32)
+__device__ __forceinline__ int key_add(float a, float c) { return __float_as_int(a + c); }
+__device__ __forceinline__ float key_const(int c) { return (float)c; }
+typedef float kconst_t;
+__device__ __forceinline__ int key_value(int kbits) { return (int)__int_as_float(kbits); }
+#else
+constexpr int kMChunks = 16;
+constexpr int kMKs = 8;
+constexpr int kChunkBits = 16;
+typedef v16i acc_t;
+constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^22), < 0x7F7F7F7F
 // 16 descriptor bits (chunk c = bits 16c .. 16c+15 = packed bytes 2c, 2c+1) to
 // 16 bytes, byte j from bit j: (nibble * 0x204081) & 0x01010101 spreads a
 // nibble's bit i to byte i; base ^ (spread << 7) flips 0x40 <-> 0xC0 (+-64).
 // Query side base 0xC0C0C0C0 (set -> +64), train side 0x40404040 (set -> -64).
-__device__ __forceinline__ v4i expand16(uint32_t bits, uint32_t base) {
+__device__ __forceinline__ v4i expand_chunk(uint32_t bits, uint32_t base) {
     v4i r;
 #pragma unroll
     for (int k = 0; k < 4; ++k) r[k] = (int)(base ^ ((((bits >> (4 * k)) & 0xFu) * 0x00204081u & 0x01010101u) << 7));
     return r;
 }
 constexpr uint32_t kExpQ = 0xC0C0C0C0u, kExpT = 0x40404040u;
+__device__ __forceinline__ acc_t mfma_chunk(v4i a, v4i b, acc_t c) {
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int key_add(int a, int c) { return a + c; }
+__device__ __forceinline__ int key_const(int c) { return c; }
+typedef int kconst_t;
+__device__ __forceinline__ int key_value(int kbits) { return kbits; }
+#endif
+constexpr int kChunkMask = kMChunks - 1;
 __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 8191); }
 
+// One stage of 64 trains against the wave's 64 queries.  Backward key of
+// register g of strip s: D + 2^20 + the query row (rowb = 2^20 + qs + 4h).
 template <bool kFull>
-__device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][8], int (&best)[2][16], int t0,
+__device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][kMKs], int (&best)[2][16], int t0,
                                          int nt, int r, int h, int rowb, int nq) {
+#if DVO_MATCH_FP4
+    const float rbf = (float)rowb;  // + goff below: exact, loop-invariant (hoisted into registers)
+#endif
 #pragma unroll 1
     for (int tt = 0; tt < kMStage / 32; ++tt) {
         const int j = t0 + 32 * tt + r;
-        const int cf = j < nt ? kKeyBase + j : kKeyNone;
-        v16i acc0 = {}, acc1 = {};
+        const kconst_t cf = key_const(j < nt ? kKeyBase + j : (DVO_MATCH_FP4 ? (1 << 30) : kKeyNone));
+        acc_t acc0 = {}, acc1 = {};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-            const v4i B = btc[(32 * tt + r) * 16 + ((2 * ks + h) ^ (r & 15))];
-            acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][ks], B, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1][ks], B, acc1, 0, 0, 0);
+        for (int ks = 0; ks < kMKs; ++ks) {
+            const v4i B = btc[(32 * tt + r) * kMChunks + ((2 * ks + h) ^ (r & kChunkMask))];
+            acc0 = mfma_chunk(A[0][ks], B, acc0);
+            acc1 = mfma_chunk(A[1][ks], B, acc1);
         }
         int cm = 0x7FFFFFFF;
+#if !DVO_MATCH_FP4
         int rb = rowb;
         asm volatile("" : "+v"(rb));  // keep rowb + goff out of 32 hoisted registers: one v_add3 per element
+#endif
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int goff = (g & 3) + 8 * (g >> 2);
-            best[0][g] = min(best[0][g], acc0[g] + cf);
-            best[1][g] = min(best[1][g], acc1[g] + cf);
+            best[0][g] = min(best[0][g], key_add(acc0[g], cf));
+            best[1][g] = min(best[1][g], key_add(acc1[g], cf));
+#if DVO_MATCH_FP4
+            int k0 = key_add(acc0[g], rbf + (float)goff), k1 = key_add(acc1[g], rbf + (float)(32 + goff));
+#else
             int k0 = acc0[g] + rb + goff, k1 = acc1[g] + rb + (32 + goff);
+#endif
             if (!kFull) {
                 k0 = rowb - kKeyBase + goff < nq ? k0 : kKeyNone;
                 k1 = rowb - kKeyBase + 32 + goff < nq ? k1 : kKeyNone;
@@ -106,7 +177,7 @@ struct NnOperands {
 // workgroup a contiguous 1/tsplit of the train stages and folds the forward
 // keys with atomicMin too (fwd pre-filled with 0x7F7F7F7F).
 __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit) {
-    __shared__ v4i bt[2][kMStage * 16];
+    __shared__ v4i bt[2][kMStage * kMChunks];
     __shared__ int colmin[2][kMStage];
     const int nwg = gridDim.x;  // a multiple of 8
     const int L0 = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
@@ -125,7 +196,7 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands
     int32_t* fwd = P.buf.nn + (int64_t)p * cap;
     int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
     const int qs = qbase + wid * 64;  // this wave's first query
-    v4i A[2][8];
+    v4i A[2][kMKs];
     int best[2][16];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -134,8 +205,11 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands
         const uint4 w1 = q < nq ? XQ[2 * (int64_t)q + 1] : make_uint4(0, 0, 0, 0);
         const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)  // chunk 2 ks + h = half h of word ks; a zero fragment past nq
-            A[s2][ks] = q < nq ? expand16(wd[ks] >> (16 * h), kExpQ) : (v4i){0, 0, 0, 0};
+        for (int ks = 0; ks < kMKs; ++ks) {  // chunk 2 ks + h; a zero fragment past nq
+            const int ch = 2 * ks + h;
+            const uint32_t bits = kChunkBits == 32 ? wd[ch] : wd[ch >> 1] >> (16 * (ch & 1));
+            A[s2][ks] = q < nq ? expand_chunk(bits, kExpQ) : (v4i){0, 0, 0, 0};
+        }
 #pragma unroll
         for (int g = 0; g < 16; ++g) best[s2][g] = 0x7FFFFFFF;
     }
@@ -150,11 +224,12 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands
     auto load_stage = [&](int st) { v = XT[(int64_t)min(st * kMStage + tr, nt - 1) * 4 + qd]; };  // clamped
     auto store_stage = [&](int st, int b) {
         const bool in = st * kMStage + tr < nt;  // zero operands past nt
+        constexpr int kPer = kMChunks / 4;       // chunks of this thread's 8 bytes
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int ch = 4 * qd + c;
-            bt[b][tr * 16 + (ch ^ (tr & 15))] =
-                in ? expand16((c < 2 ? v.x : v.y) >> (16 * (c & 1)), kExpT) : (v4i){0, 0, 0, 0};
+        for (int c = 0; c < kPer; ++c) {
+            const int ch = kPer * qd + c;
+            const uint32_t bits = kChunkBits == 32 ? (c == 0 ? v.x : v.y) : (c < 2 ? v.x : v.y) >> (16 * (c & 1));
+            bt[b][tr * kMChunks + (ch ^ (tr & kChunkMask))] = in ? expand_chunk(bits, kExpT) : (v4i){0, 0, 0, 0};
         }
         if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;
     };
@@ -172,7 +247,7 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands
         __syncthreads();
         const int t = st * kMStage + threadIdx.x;
         if (threadIdx.x < kMStage && t < nt && colmin[cur][threadIdx.x] != 0x7FFFFFFF)
-            atomicMin(&bwd[t], key_old(colmin[cur][threadIdx.x]));
+            atomicMin(&bwd[t], key_old(key_value(colmin[cur][threadIdx.x])));
     }
     // forward: minimum over the 32 lanes of each half (they hold the 32 columns)
 #pragma unroll
@@ -185,9 +260,9 @@ __global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands
             const int qr = qs + 32 * s2 + (g & 3) + 8 * (g >> 2) + 4 * h;
             if (r == g && qr < nq) {
                 if (tsplit > 1) {
-                    if (st0 < nst) atomicMin(&fwd[qr], key_old(vv));
+                    if (st0 < nst) atomicMin(&fwd[qr], key_old(key_value(vv)));
                 } else {
-                    fwd[qr] = nt > 0 ? key_old(vv) : -1;
+                    fwd[qr] = nt > 0 ? key_old(key_value(vv)) : -1;
                 }
             }
         }
