@@ -124,6 +124,9 @@ __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 
 template <bool kFull>
 __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][kMKs], int (&best)[2][16], int t0,
                                          int nt, int r, int h, int rowb, int nq) {
+#ifndef DVO_MATCH_HOIST
+#define DVO_MATCH_HOIST 1
+#endif
 #if DVO_MATCH_FP4
     const float rbf = (float)rowb;  // + goff below: exact, loop-invariant (hoisted into registers)
 #endif
@@ -148,7 +151,11 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
             const int goff = (g & 3) + 8 * (g >> 2);
             best[0][g] = min(best[0][g], key_add(acc0[g], cf));
             best[1][g] = min(best[1][g], key_add(acc1[g], cf));
-#if DVO_MATCH_FP4
+#if DVO_MATCH_FP4 && !DVO_MATCH_HOIST
+            float rb = rbf;
+            asm volatile("" : "+v"(rb));  // not hoisted: 32 fewer live registers, one more add per element
+            int k0 = key_add(acc0[g], rb + (float)goff), k1 = key_add(acc1[g], rb + (float)(32 + goff));
+#elif DVO_MATCH_FP4
             int k0 = key_add(acc0[g], rbf + (float)goff), k1 = key_add(acc1[g], rbf + (float)(32 + goff));
 #else
             int k0 = acc0[g] + rb + goff, k1 = acc1[g] + rb + (32 + goff);
@@ -176,7 +183,12 @@ struct NnOperands {
 // tsplit > 1 (the per-call path: one pair, so a short grid) gives each
 // workgroup a contiguous 1/tsplit of the train stages and folds the forward
 // keys with atomicMin too (fwd pre-filled with 0x7F7F7F7F).
-__global__ __launch_bounds__(256) void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit) {
+// Resident waves per SIMD asked of the compiler (165 VGPRs unconstrained = 3).
+#ifndef DVO_MATCH_WAVES
+#define DVO_MATCH_WAVES 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DVO_MATCH_WAVES)))
+void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit) {
     __shared__ v4i bt[2][kMStage * kMChunks];
     __shared__ int colmin[2][kMStage];
     const int nwg = gridDim.x;  // a multiple of 8
