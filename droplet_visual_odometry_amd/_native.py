@@ -132,6 +132,7 @@ _SIGNATURES = {
     "dvo_test_retain_best": ([_vp, _vp, _c, _c, _c, _c, _vp, _ip], _c),
     "dvo_test_update_num_iters": ([_vp, _d, _vp, _c, _c, _c, _vp], _c),
     "dvo_test_five_point": ([_vp, _vp, _vp, _vp, _ip], _c),
+    "dvo_test_sampson": ([_vp, _vp, _vp, _c, ctypes.c_float, _vp, _vp], _c),
     "dvo_test_ransac_subsets": ([_vp, _c, _c, _vp], _c),
     "dvo_test_ransac_replay": ([_vp, _vp, _vp, _c, _c, _d, _c, _vp], _c),
 }

@@ -1625,6 +1625,25 @@ int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double
     return DVO_OK;
 }
 
+int dvo_test_sampson(dvo_ctx* ctx, const double* E, const double* pts, int n, float t, int8_t* dec,
+                     uint8_t* exact) {
+    if (!ctx || !E || n < 0 || (n > 0 && (!pts || !dec || !exact))) return DVO_EINVAL;
+    if (n == 0) return DVO_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void *dE, *dp, *dd, *dx;
+    int rc;
+    if ((rc = scratch(ctx, 26, 9 * 8, &dE)) || (rc = scratch(ctx, 27, (size_t)n * 32, &dp)) ||
+        (rc = scratch(ctx, 28, (size_t)n, &dd)) || (rc = scratch(ctx, 29, (size_t)n, &dx)))
+        return rc;
+    HIP_TRY(hipMemcpy(dE, E, 9 * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(dp, pts, (size_t)n * 32, hipMemcpyHostToDevice));
+    HIP_TRY(launch_test_sampson((const double*)dE, (const double*)dp, n, t, (int8_t*)dd, (uint8_t*)dx, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(dec, dd, (size_t)n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(exact, dx, (size_t)n, hipMemcpyDeviceToHost));
+    return DVO_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

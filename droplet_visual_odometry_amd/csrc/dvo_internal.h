@@ -366,5 +366,7 @@ hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int
 hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s);
 hipError_t launch_test_ransac_replay(const GeomArgs& g, hipStream_t s);
 hipError_t launch_test_five_point(const double* d_q, double* d_models, int* d_n, hipStream_t s);
+hipError_t launch_test_sampson(const double* d_E, const double* d_pts, int n, float t, int8_t* d_dec, uint8_t* d_ex,
+                               hipStream_t s);
 
 }  // namespace dvo

@@ -21,6 +21,7 @@
 // Every double expression mirrors oracle/geometry.cpp operation for operation
 // (compiled with -ffp-contract=off), so E, R and t are bit-identical to it.
 #include "dvo_internal.h"
+#include "sampson.h"
 
 #include <cfloat>
 
@@ -927,39 +928,6 @@ __device__ __forceinline__ int five_point(const double (&q)[5][4], double* model
     return fp_stage_c(R, models);
 }
 
-// EMEstimatorCallback::computeError (five-point.cpp): err = (float)(num / den)
-// with num = (x2' E x1)^2 and den = the four squared epipolar terms; the
-// inlier test err <= t (ptsetreg.cpp findInliers), decided without the f64
-// division for all but a sliver of points.  With nf = fl32(num),
-// df = fl32(den), s = fl32(t * df) (relative errors <= 2^-24 each while the
-// values are normal floats, which the range checks on t and s guarantee):
-//   nf < fl32(s * (1 - 2^-20))  =>  num < t * den  =>  fl64(num / den) <= t (RN is
-//                                   monotone and t is a double), so (float) <= t;
-//   nf > fl32(s * (1 + 2^-20))  =>  num / den > t (1 + 2^-21)  =>  the double
-//                                   quotient is past t's rounding midpoint
-//                                   (half an ulp <= t 2^-24), so (float) > t.
-// (nf zero, denormal or +inf only strengthens either inequality.)  Otherwise,
-// and for NaN, the exact division decides.  Bit-identical inlier sets.
-__device__ __forceinline__ bool sampson_inlier(const double* E, double x1, double y1, double x2, double y2, float t,
-                                               bool fast_ok) {
-    double ex0 = E[0] * x1 + E[1] * y1 + E[2] * 1.;
-    double ex1 = E[3] * x1 + E[4] * y1 + E[5] * 1.;
-    double ex2 = E[6] * x1 + E[7] * y1 + E[8] * 1.;
-    double et0 = E[0] * x2 + E[3] * y2 + E[6] * 1.;
-    double et1 = E[1] * x2 + E[4] * y2 + E[7] * 1.;
-    double x2tEx1 = x2 * ex0 + y2 * ex1 + 1. * ex2;
-    double a = ex0 * ex0, b = ex1 * ex1, c = et0 * et0, d = et1 * et1;
-    const double num = x2tEx1 * x2tEx1, den = a + b + c + d;
-    if (fast_ok) {
-        const float nf = (float)num, s = t * (float)den;
-        if (s >= 1e-30f && s <= 1e30f) {
-            if (nf < s * (1.f - 0x1p-20f)) return true;
-            if (nf > s * (1.f + 0x1p-20f)) return false;
-        }
-    }
-    return (float)(num / den) <= t;
-}
-
 __device__ int ransac_update_num_iters(double p, double ep, int model_points, int max_iters) {
     p = p > 0. ? p : 0.;
     p = p < 1. ? p : 1.;
@@ -1029,6 +997,9 @@ __device__ __forceinline__ void dk_priority() {
 #endif
 #ifndef DVO_SCORE_HYPS_CALL
 #define DVO_SCORE_HYPS_CALL 2  // drop-in pairs/s (profiles/r02z_ab_dropin_score_hyps.txt): 1 620, 2 626, 4 611, 16 610
+#endif
+#ifndef DVO_SCORE_F32
+#define DVO_SCORE_F32 1  // single-precision decision with the f64 test for the undecided (SampsonF32)
 #endif
 constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
@@ -1570,18 +1541,27 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     const int hn = min(HYPS, S.h1 - hb);
     const int m = S.m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#if !DVO_SCORE_F32
     __shared__ double s_pts[kScoreChunk * 4];
+#endif
     __shared__ double s_E[HYPS * 10 * 9];
     __shared__ int s_pref[HYPS + 1];
     __shared__ int s_cnt[HYPS * 10];
+#if DVO_SCORE_F32
+    __shared__ float4 s_ptf[kScoreChunk];
+    __shared__ uint16_t s_und[kScoreNT / 64][kScoreChunk];  // per wave: undecided points of its model
+#endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
-    if (tid == 0) {
-        int acc = 0;
-        for (int i = 0; i < hn; ++i) {
-            s_pref[i] = acc;
-            acc += g.nmod[hbase + i];
+    static_assert(HYPS <= 64, "one wave prefixes the model counts");
+    if (tid < 64) {  // model counts of the block's hypotheses: one load each, a wave prefix sum
+        const int c = tid < hn ? g.nmod[hbase + tid] : 0;
+        int x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
         }
-        s_pref[hn] = acc;
+        if (tid <= hn) s_pref[tid] = x - c;
     }
     __syncthreads();
     const int T = s_pref[hn];
@@ -1599,7 +1579,14 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     for (int c0 = 0; c0 < m; c0 += kScoreChunk) {
         const int cn = min(kScoreChunk, m - c0);
         __syncthreads();
+#if !DVO_SCORE_F32
         for (int e = tid; e < cn * 4; e += kScoreNT) s_pts[e] = npts[(int64_t)c0 * 4 + e];
+#else
+        for (int e = tid; e < cn; e += kScoreNT) {
+            const double* q = npts + (int64_t)(c0 + e) * 4;
+            s_ptf[e] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+        }
+#endif
         __syncthreads();
         // one wave per model (2 or 4 models per wave pass over the chunk, reading each point
         // once, measured slower: 73.0 K vs 72.6 / 71.4 K frames/s, profiles/r02w_ab_score_dk.txt)
@@ -1608,10 +1595,42 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
             int cnt = 0;
+#if DVO_SCORE_F32
+            // undecided points of this model queue in the wave's LDS list and take the f64
+            // test together afterwards (64 per pass, instead of a divergent f64 pass for every
+            // 64 points that hold one)
+            const SampsonF32 sf(Ed, fast_ok);
+            uint16_t* und = s_und[wid];
+            int nu = 0;
+            for (int j = lane; j < cn; j += 64) {
+                const float4 pf = s_ptf[j];
+                const int d = sf.decide(pf.x, pf.y, pf.z, pf.w, t);
+                cnt += __popcll(__ballot(d == 1));
+#ifndef DVO_EXP_SCORE_NO_F64  // timing experiment only: undecided points counted as outliers
+                const unsigned long long ub = __ballot(d < 0);
+                if (d < 0) und[nu + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ub >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)ub, 0u))] =
+                    (uint16_t)j;
+                nu += __popcll(ub);
+#endif
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int u0 = 0; u0 < nu; u0 += 64) {  // the f64 coordinates from L2
+                bool in = false;
+                if (u0 + lane < nu) {
+                    const double* pt = npts + (int64_t)(c0 + und[u0 + lane]) * 4;
+                    in = sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok);
+                }
+                cnt += __popcll(__ballot(in));
+            }
+#else
             for (int j = lane; j < cn; j += 64) {
                 const double* pt = s_pts + j * 4;
                 cnt += __popcll(__ballot(sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok)));
             }
+#endif
             if (lane == 0) s_cnt[e] += cnt;
         }
     }
@@ -2304,6 +2323,27 @@ hipError_t launch_test_update_num_iters(double p, const double* d_ep, int n, int
                                         int32_t* d_out, hipStream_t s) {
     hipLaunchKernelGGL(test_update_num_iters_kernel, dim3((n + 255) / 256), dim3(256), 0, s, p, d_ep, n, model_points,
                        max_iters, d_out);
+    return hipGetLastError();
+}
+
+// SampsonF32 against sampson_inlier on one model and n points (test hook):
+// dec[i] = the f32 decision (1 / 0 / -1 undecided), ex[i] = the f64 decision.
+__global__ __launch_bounds__(256) void test_sampson_kernel(const double* E, const double* pts, int n, float t,
+                                                           int8_t* dec, uint8_t* ex) {
+    double Ed[9];
+    for (int k = 0; k < 9; ++k) Ed[k] = E[k];
+    const bool fast_ok = t >= FLT_MIN;
+    const SampsonF32 sf(Ed, fast_ok);
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const double* q = pts + (int64_t)i * 4;
+        dec[i] = (int8_t)sf.decide((float)q[0], (float)q[1], (float)q[2], (float)q[3], t);
+        ex[i] = sampson_inlier(Ed, q[0], q[1], q[2], q[3], t, fast_ok);
+    }
+}
+
+hipError_t launch_test_sampson(const double* d_E, const double* d_pts, int n, float t, int8_t* d_dec, uint8_t* d_ex,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(test_sampson_kernel, dim3(1), dim3(256), 0, s, d_E, d_pts, n, t, d_dec, d_ex);
     return hipGetLastError();
 }
 

@@ -257,6 +257,18 @@ def test_five_point(q1, q2, ctx=None):
     return models[:9 * n.value].reshape(n.value, 3, 3).copy()
 
 
+def test_sampson(E, pts, t, ctx=None):
+    """Device f32 Sampson decision (1 / 0 / -1 undecided) and the f64 test, per point."""
+    c = _ctx(ctx)
+    E = np.ascontiguousarray(E, np.float64).reshape(9)
+    pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 4)
+    n = len(pts)
+    dec = np.zeros(n, np.int8)
+    ex = np.zeros(n, np.uint8)
+    c.check(c.lib.dvo_test_sampson(c.h, ptr(E), ptr(pts), n, float(t), ptr(dec), ptr(ex)))
+    return dec, ex.astype(bool)
+
+
 # ---- image pre-processing (visual_odometry_v3.py:110-135, SURVEY.md §8f rank 1) ----
 def get_optimal_new_camera_matrix(K, dist, size, alpha=1.0, new_size=None) -> np.ndarray:
     """cv.getOptimalNewCameraMatrix(K, dist, size, alpha, new_size)[0] (v3:117)."""

@@ -310,6 +310,12 @@ int dvo_test_ransac_replay(dvo_ctx* ctx, const int32_t* nmod, const int32_t* cnt
                            int max_iters, int32_t* out);
 /* 5-point kernel on one sample of 5 normalised correspondences. */
 int dvo_test_five_point(dvo_ctx* ctx, const double* q1, const double* q2, double* models, int* n);
+/* The batched RANSAC score's single-precision Sampson decision on one model E
+ * (9 doubles) and n normalised correspondences (n x {x1, y1, x2, y2}) at the
+ * squared threshold t: dec[i] = 1 inlier / 0 outlier / -1 left to the f64 test,
+ * exact[i] = the f64 test (computeError, err <= t). */
+int dvo_test_sampson(dvo_ctx* ctx, const double* E, const double* pts, int n, float t, int8_t* dec,
+                     uint8_t* exact);
 
 #ifdef __cplusplus
 }
