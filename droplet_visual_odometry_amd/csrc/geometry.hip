@@ -1543,13 +1543,14 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #if !DVO_SCORE_F32
     __shared__ double s_pts[kScoreChunk * 4];
-#endif
     __shared__ double s_E[HYPS * 10 * 9];
+#endif
     __shared__ int s_pref[HYPS + 1];
     __shared__ int s_cnt[HYPS * 10];
 #if DVO_SCORE_F32
     __shared__ float4 s_ptf[kScoreChunk];
-    __shared__ uint16_t s_und[kScoreNT / 64][kScoreChunk];  // per wave: undecided points of its model
+    __shared__ float s_sf[HYPS * 10][12];  // SampsonF32 of each model: e[9], mk, ok
+    __shared__ int s_moff[HYPS * 10];      // the model's offset in g.models (the f64 test)
 #endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
     static_assert(HYPS <= 64, "one wave prefixes the model counts");
@@ -1565,16 +1566,34 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     }
     __syncthreads();
     const int T = s_pref[hn];
+#if !DVO_SCORE_F32
     for (int e = tid; e < T * 9; e += kScoreNT) {
         const int mi = e / 9, k = e - mi * 9;
         int h = 0;
         while (h + 1 < hn && s_pref[h + 1] <= mi) ++h;
         s_E[e] = g.models[(hbase + h) * 90 + (mi - s_pref[h]) * 9 + k];
     }
+#endif
     for (int e = tid; e < T; e += kScoreNT) s_cnt[e] = 0;
     const double thr = g.threshold / ((g.fx + g.fy) / 2);
     const float t = (float)(thr * thr);
     const bool fast_ok = t >= FLT_MIN;  // the division-free test needs t normal
+#if DVO_SCORE_F32
+    for (int e = tid; e < T; e += kScoreNT) {  // once per model, not per chunk
+        int h = 0;
+        while (h + 1 < hn && s_pref[h + 1] <= e) ++h;
+        const int off = (int)((hbase + h) * 90 + (e - s_pref[h]) * 9 - hbase * 90);
+        s_moff[e] = off;
+        double Ed[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Ed[k] = g.models[hbase * 90 + off + k];
+        const SampsonF32 sf(Ed, fast_ok);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s_sf[e][k] = sf.e[k];
+        s_sf[e][9] = sf.mk;
+        s_sf[e][10] = sf.ok ? 1.f : 0.f;
+    }
+#endif
     const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
     for (int c0 = 0; c0 < m; c0 += kScoreChunk) {
         const int cn = min(kScoreChunk, m - c0);
@@ -1591,41 +1610,45 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         // one wave per model (2 or 4 models per wave pass over the chunk, reading each point
         // once, measured slower: 73.0 K vs 72.6 / 71.4 K frames/s, profiles/r02w_ab_score_dk.txt)
         for (int e = wid; e < T; e += kScoreNT / 64) {
+            int cnt = 0;
+#if DVO_SCORE_F32
+            // undecided points (a sliver) are marked per lane and take the f64 test after the
+            // chunk, only in the waves that have one
+            SampsonF32 sf;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) sf.e[k] = s_sf[e][k];
+            sf.mk = s_sf[e][9];
+            sf.ok = s_sf[e][10] != 0.f;
+            uint32_t umask = 0;
+#pragma unroll
+            for (int k = 0; k < kScoreChunk / 64; ++k) {
+                const int j = lane + 64 * k;
+                if (64 * k >= cn) break;  // wave-uniform
+                const float4 pf = s_ptf[min(j, cn - 1)];
+                const int d = j < cn ? sf.decide(pf.x, pf.y, pf.z, pf.w, t) : 0;
+                cnt += __popcll(__ballot(d == 1));
+                umask |= (uint32_t)(d < 0) << k;
+            }
+#ifndef DVO_EXP_SCORE_NO_F64  // timing experiment only: undecided points counted as outliers
+            if (__ballot(umask != 0)) {
+                double Ed[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Ed[k] = g.models[hbase * 90 + s_moff[e] + k];
+                for (int k = 0; k < kScoreChunk / 64; ++k) {  // the f64 model and coordinates from L2
+                    if (__ballot((umask >> k) & 1u) == 0) continue;  // wave-uniform: usually one k has any
+                    bool in = false;
+                    if ((umask >> k) & 1u) {
+                        const double* pt = npts + (int64_t)(c0 + lane + 64 * k) * 4;
+                        in = sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok);
+                    }
+                    cnt += __popcll(__ballot(in));
+                }
+            }
+#endif
+#else
             double Ed[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
-            int cnt = 0;
-#if DVO_SCORE_F32
-            // undecided points of this model queue in the wave's LDS list and take the f64
-            // test together afterwards (64 per pass, instead of a divergent f64 pass for every
-            // 64 points that hold one)
-            const SampsonF32 sf(Ed, fast_ok);
-            uint16_t* und = s_und[wid];
-            int nu = 0;
-            for (int j = lane; j < cn; j += 64) {
-                const float4 pf = s_ptf[j];
-                const int d = sf.decide(pf.x, pf.y, pf.z, pf.w, t);
-                cnt += __popcll(__ballot(d == 1));
-#ifndef DVO_EXP_SCORE_NO_F64  // timing experiment only: undecided points counted as outliers
-                const unsigned long long ub = __ballot(d < 0);
-                if (d < 0) und[nu + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ub >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)ub, 0u))] =
-                    (uint16_t)j;
-                nu += __popcll(ub);
-#endif
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int u0 = 0; u0 < nu; u0 += 64) {  // the f64 coordinates from L2
-                bool in = false;
-                if (u0 + lane < nu) {
-                    const double* pt = npts + (int64_t)(c0 + und[u0 + lane]) * 4;
-                    in = sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok);
-                }
-                cnt += __popcll(__ballot(in));
-            }
-#else
             for (int j = lane; j < cn; j += 64) {
                 const double* pt = s_pts + j * 4;
                 cnt += __popcll(__ballot(sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok)));

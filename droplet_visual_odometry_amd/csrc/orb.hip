@@ -1482,15 +1482,8 @@ constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padd
 #endif
 constexpr int kDBRows = 10, kDBSeg = 4, kDBRaw = kDBRows + 6;  // output rows per lane segment, segments, raw rows
 
-// DVO_DESCRIBE_BRANCHFREE: every lane stores every row, the ones outside the patch (halo words,
-// lanes 52..63, rows past 38) into a per-wave junk word, so the row has no divergent branch
-// (the compiler otherwise sinks the horizontal taps into the store's branch: exec-mask SALU and
-// a scalar-constant rematerialisation per row).
-#ifndef DVO_DESCRIBE_BRANCHFREE
-#define DVO_DESCRIBE_BRANCHFREE 1
-#endif
 __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw], uint8_t* patch_slot, int s, int wc,
-                                                   bool he, uint32_t* junk) {
+                                                   bool he) {
     const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
     const uint32_t R = he ? 0x7FFFu : 0x8000u;
     u16x2 lo[7], hi[7];
@@ -1536,14 +1529,8 @@ __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw]
         const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0C0C0602u),
                                                     __builtin_amdgcn_perm(s1, s0, 0x0C0C0602u), 0x05040100u);
         const int i = kDBRows * s + (r - 6);  // patch row
-#if DVO_DESCRIBE_BRANCHFREE
-        const bool in = s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH;
-        *(in ? reinterpret_cast<uint32_t*>(patch_slot + i * kDPW) + (wc - 1) : junk) = word;
-#else
-        (void)junk;
         if (s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH)
             reinterpret_cast<uint32_t*>(patch_slot + i * kDPW)[wc - 1] = word;
-#endif
     }
 }
 
@@ -1552,7 +1539,6 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t icw[4][kICR][kICW];
     __shared__ float s_ang[kDKB], s_ca[kDKB], s_sa[kDKB];
     __shared__ int s_pc[kDKB];  // offset of the keypoint's centre in its patch
-    __shared__ uint32_t s_junk[4][64];  // describe_blur_rows: stores of lanes outside the patch
     // 1-D grid: block b runs on XCD b & 7, and XCD x takes frames x, x + 8, ...
     // in turn, so one frame's keypoint windows meet in one L2 (and its
     // descriptors are written there for the matcher): 61.9-62.7 K -> 64.3 K frames/s
@@ -1680,7 +1666,7 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
 #if DVO_DESCRIBE_BLUR
         describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc,
-                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w, &s_junk[wv][lane]);
+                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w);
 #else
 #pragma unroll
         for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pvs[kk][t];

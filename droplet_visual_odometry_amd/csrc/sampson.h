@@ -67,6 +67,7 @@ DVO_HD inline bool sampson_inlier(const double* E, double x1, double y1, double 
 struct SampsonF32 {
     float e[9], mk;
     bool ok;
+    SampsonF32() = default;
     DVO_HD SampsonF32(const double* E, bool t_ok) {
         float M = 0.f;
 #pragma unroll
