@@ -39,12 +39,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
 VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
-PMC_TRAFFIC = "r03t_pmc_traffic.json"  # tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes of the kernels
+PMC_TRAFFIC = "r03z_pmc_traffic.json"  # tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes of the kernels
 # FP64 vector peak: 78.6 TFLOP/s, AMD's MI355X data-sheet figure (MI355X_MICROARCH.md lists no f64 row).  It is
 # the wave64 f64 FMA issue rate: 16 lanes per cycle per SIMD (a wave64 f64 instruction per 4 cycles) x 2 FLOP x
 # 1024 SIMDs x 2.4 GHz.
 F64_PEAK_TFLOPS = 78.6
-PMC_F64 = "r03t_pmc_f64.json"  # tools/pmc_stall_f64.sh + tools/pmc_f64.py: f64 VALU instructions per kernel
+PMC_F64 = "r03z_pmc_f64.json"  # tools/pmc_stall_f64.sh + tools/pmc_f64.py: f64 VALU instructions per kernel
 
 
 def parse():
