@@ -1480,10 +1480,28 @@ constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padd
 #ifndef DVO_DESCRIBE_BLUR
 #define DVO_DESCRIBE_BLUR 1
 #endif
+// Only the pixels the rotated pattern can sample are blurred: pattern points lie within
+// r = 18.385 of the centre (|x|, |y| <= 13), so a sample rounds to |dy| <= 18 and, in row dy,
+// |dx| <= floor(sqrt(r^2 - (|dy| - 1/2)^2) + 1/2) (r for dy = 0): 6, 8, 10, .. 18 .. 6 (equal to
+// the extents of cvRound over a 2e5-step angle sweep).  Five bands of 8 patch rows
+// (dy = -18 + 8s .. -11 + 8s) take 11, 12, 12, 12 and 9 lanes (the band's words at its largest
+// |dx| for any keypoint alignment, plus a halo word each side): 56 lanes, 8 rows each, where the
+// full 39 x 44 window needed 52 lanes x 10 rows.  DVO_DESCRIBE_DISK=0: the full window.
+#ifndef DVO_DESCRIBE_DISK
+#define DVO_DESCRIBE_DISK 1
+#endif
+#if DVO_DESCRIBE_DISK
+constexpr int kDBRows = 8, kDBSeg = 5, kDBRaw = kDBRows + 6;  // output rows per band, bands, raw rows
+constexpr int kDBRow0 = 1;                                     // patch row of band 0's first row (dy = -18)
+constexpr int kDBBase[kDBSeg + 1] = {0, 11, 23, 35, 47, 56};    // first lane of each band
+constexpr int kDBHalfW[kDBSeg] = {15, 18, 18, 18, 12};          // largest |dx| in the band
+#else
 constexpr int kDBRows = 10, kDBSeg = 4, kDBRaw = kDBRows + 6;  // output rows per lane segment, segments, raw rows
+constexpr int kDBRow0 = 0;
+#endif
 
 __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw], uint8_t* patch_slot, int s, int wc,
-                                                   bool he) {
+                                                   bool he, bool st) {
     const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
     const uint32_t R = he ? 0x7FFFu : 0x8000u;
     u16x2 lo[7], hi[7];
@@ -1528,8 +1546,8 @@ __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw]
         s3 = min(s3, 0xFFFFFFu);
         const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0C0C0602u),
                                                     __builtin_amdgcn_perm(s1, s0, 0x0C0C0602u), 0x05040100u);
-        const int i = kDBRows * s + (r - 6);  // patch row
-        if (s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH)
+        const int i = kDBRow0 + kDBRows * s + (r - 6);  // patch row
+        if (st && s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH)
             reinterpret_cast<uint32_t*>(patch_slot + i * kDPW)[wc - 1] = word;
     }
 }
@@ -1599,7 +1617,18 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
 #if DVO_DESCRIBE_BLUR
     uint32_t ivs[kDKW][5], pvs[kDKW][kDBRaw];
+#if DVO_DESCRIBE_DISK
+    int db_s = 0;
+#pragma unroll
+    for (int q = 1; q < kDBSeg; ++q) db_s += lane >= kDBBase[q];
+    const int db_k = lane - kDBBase[db_s];  // lanes >= 56: band 4 past its words (loads in range, no store)
+    const int db_hw = db_s == 0 ? kDBHalfW[0] : db_s == 4 ? kDBHalfW[4] : kDBHalfW[1];
+    const bool db_st = db_k >= 1 && db_k <= kDBBase[db_s + 1] - kDBBase[db_s] - 2;  // not a band halo word
+    int db_wcs[kDKW];
+#else
     const int db_s = lane / 13, db_wc = lane - 13 * db_s;  // lanes >= 52: segment 4 (loads in range, no store)
+    constexpr bool db_st = true;
+#endif
 #else
     uint32_t ivs[kDKW][5], pvs[kDKW][7];
 #endif
@@ -1632,7 +1661,14 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #if DVO_DESCRIBE_BLUR
         {  // raw rows cyb - 22 + 10 s .. + 15 of word db_wc of [a0 - 4, a0 + 48)
             const int sr = min(db_s, kDBSeg - 1);
-            const uint8_t* rw = level_ptr(P, f, l) + (int64_t)(cyb - kDPR - 3 + kDBRows * sr) * step + a0 - 4 + 4 * db_wc;
+#if DVO_DESCRIBE_DISK
+            // the band's first word: the one left of the word holding cx - halfwidth (raw word
+            // index ((x - a0) >> 2) + 1); <= 12 for every lane of the band
+            const int db_wc = min(((cxb - db_hw - a0) >> 2) + db_k, 12);
+            db_wcs[kk] = db_wc;
+#endif
+            const uint8_t* rw = level_ptr(P, f, l) + (int64_t)(cyb - kDPR - 3 + kDBRow0 + kDBRows * sr) * step +
+                                a0 - 4 + 4 * db_wc;
 #pragma unroll
             for (int t = 0; t < kDBRaw; ++t) pvs[kk][t] = *reinterpret_cast<const uint32_t*>(rw + (int64_t)t * step);
             (void)bl;
@@ -1665,8 +1701,11 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #pragma unroll
         for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
 #if DVO_DESCRIBE_BLUR
+#if DVO_DESCRIBE_DISK
+        const int db_wc = db_wcs[kk];
+#endif
         describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc,
-                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w);
+                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w, db_st);
 #else
 #pragma unroll
         for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pvs[kk][t];
