@@ -696,6 +696,8 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
     const int c_col = 4 + 4 * (lane & 31), c_hi = xlast - bx + 1 - c_col;
     const uint32_t c_vm = (c_col == 4 ? 0xFFFF0000u : 0xFFFFFFFFu) &
                           (c_hi >= 4 ? 0xFFFFFFFFu : c_hi <= 0 ? 0u : (1u << (8 * c_hi)) - 1u);
+    // the same as a 4-bit pixel mask (bit k <-> byte k)
+    const uint32_t c_vm4 = (c_vm & 1u) | ((c_vm >> 7) & 2u) | ((c_vm >> 14) & 4u) | ((c_vm >> 21) & 8u);
     const uint32_t thr2 = (uint32_t)thr * 0x10001u;
     // Words past the row end are never read by the FAST tests (x + 3 <= w - 1): the buffer
     // load returns whatever lies there (or 0 past the level).  The row offset goes in the
@@ -789,11 +791,16 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
                                                   as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C030C01)),
                                                   as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C060C04)),
                                                   as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C040C02)), thr2);
-                // byte k of pm nonzero <=> pixel k passes and is a score pixel of this tile; bit k of
-                // msk the same (bit 7 of each byte <- byte != 0, then the 4 bits gathered by one multiply)
-                const uint32_t pm = (r0p | (r1p << 8)) & (sr < nsr ? c_vm : 0u);
-                const uint32_t nzb = ((((pm & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | pm) >> 7) & 0x01010101u;
-                const uint32_t msk = (nzb * 0x10204080u) >> 28;
+                // bit k of msk <=> pixel k passes and is a score pixel of this tile: each half of
+                // r0p (pixels 0, 2) and r1p (1, 3) is <= 255 and nonzero iff the pixel passes, so a
+                // packed min with 1 gives its bit; (p0 | p1 << 1) in bits 0-1, (p2 | p3 << 1) in 16-17
+                // (LLVM folds a packed min with 1 into per-half compares and selects: v_pk_min_u16
+                // written out keeps it at one instruction per pair)
+                uint32_t b0, b1;
+                asm("v_pk_min_u16 %0, %1, %2" : "=v"(b0) : "v"(r0p), "v"(0x00010001u));
+                asm("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r1p), "v"(0x00010001u));
+                const uint32_t m2 = b0 | (b1 << 1);
+                const uint32_t msk = (m2 | (m2 >> 14)) & (sr < nsr ? c_vm4 : 0u);
                 // one entry per word with a passing pixel: (word index | mask << 12)
                 const bool any = msk != 0;
                 const unsigned long long bal = __ballot(any);
