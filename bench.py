@@ -39,12 +39,28 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
 VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
-PMC_TRAFFIC = "r03z_pmc_traffic.json"  # tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes of the kernels
+# PMC documents (tools/profile_round.sh: calibrated FETCH/WRITE_SIZE + SQ passes; tools/pmc_stall_f64.sh +
+# tools/pmc_f64.py: f64 VALU instructions per kernel) are looked up under profiles/ by the workload they were
+# collected on: the newest round tag whose config matches (width, height, nfeatures) wins (pmc_doc).
+PMC_TRAFFIC_GLOB = "r*_pmc_traffic*.json"
+PMC_F64_GLOB = "r*_pmc_f64*.json"
 # FP64 vector peak: 78.6 TFLOP/s, AMD's MI355X data-sheet figure (MI355X_MICROARCH.md lists no f64 row).  It is
 # the wave64 f64 FMA issue rate: 16 lanes per cycle per SIMD (a wave64 f64 instruction per 4 cycles) x 2 FLOP x
 # 1024 SIMDs x 2.4 GHz.
 F64_PEAK_TFLOPS = 78.6
-PMC_F64 = "r03z_pmc_f64.json"  # tools/pmc_stall_f64.sh + tools/pmc_f64.py: f64 VALU instructions per kernel
+# The kernels of each HIP-event stage (include/dvo.h DVO_NSTAGES; api.cpp run_stream / launch_geometry).
+STAGE_KERNELS = {
+    "pyramid": ["resize_level_lds_kernel"],
+    "blur": ["blur_kernel"],
+    "fast": ["fast_strip_kernel"],
+    "select_harris": ["select_fast_kernel", "harris_kernel", "select_harris_kernel"],
+    "describe": ["describe_kernel"],
+    "match": ["nn_mfma_kernel", "crosscheck_stream_kernel"],
+    "ransac": ["normalize_kernel", "ransac_"],
+    "recover_pose": ["pose_decompose_kernel", "pose_count_kernel", "pose_pick_kernel", "records_kernel"],
+    "pose_tail": ["pose_tail_kernel", "pose_chain_kernel"],
+}
+PAIR_STAGES = ("match", "ransac", "recover_pose", "pose_tail")  # units are pairs (B), the rest frames (B + 1)
 
 
 def parse():
@@ -71,6 +87,12 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight: each on its own dvo_stream / HIP stream, so one batch's "
                          "serial RANSAC tail overlaps the next batch's ORB")
+    ap.add_argument("--no-ref-equivalent", action="store_true",
+                    help="skip the reference-equivalent leg (both frames of every pair detected, GPU and CPU)")
+    ap.add_argument("--no-host-fed", action="store_true",
+                    help="skip the host-fed leg (pinned host frames, async H2D on a copy stream)")
+    ap.add_argument("--pose-check-32", type=int, default=24,
+                    help="pairs of the OpenCV 3.2-semantics pose check against the oracle (0 = skip)")
     return ap.parse_args()
 
 
@@ -194,41 +216,29 @@ def main():
     ok = int(np.sum(recs["status"] == 0))
     roofline = None
     if stage_ms and calls:
-        sb = stage_bytes(W, H, N, m_avg)
         per_call = {k: v / calls for k, v in stage_ms.items()}
-        # roofline of the dominant single-kernel stage (one launch per step, so the
-        # HIP-event time on the library's stream is that kernel's duration)
-        single = {"fast": "fast_strip_kernel", "blur": "blur_kernel", "describe": "describe_kernel"}
-        dom = max(single, key=lambda k: per_call.get(k, 0.0))
-        bytes_per_launch = sb[dom] * (B + 1)
-        achieved = bytes_per_launch / (per_call[dom] * 1e-3) / 1e9
-        pmc = pmc_counts(single[dom], W, H, N, B)
-        valu = None
-        if pmc and pmc["valu_insts"]:
-            va = pmc["valu_insts"] / (per_call[dom] * 1e-3)
-            valu = {"achieved": round(va / 1e9, 3), "peak": VALU_PEAK_WIPS / 1e9, "unit": "G wave-instructions/s",
-                    "frac": round(va / VALU_PEAK_WIPS, 6), "insts_per_launch": round(pmc["valu_insts"]),
-                    "note": "SQ_INSTS_VALU per launch / the launch's HIP-event time; peak = one wave64 VALU "
-                            "instruction per 2 cycles per SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)"}
-        roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": pmc["traffic"] if pmc else None,
-                    "traffic_raw": pmc["traffic_raw"] if pmc else None,
-                    "traffic_calibrated": pmc["calibrated"] if pmc else None,
-                    "traffic_source": pmc["source"] if pmc else None,
-                    "valu": valu, "valu_frac": valu["frac"] if valu else None,
-                    "kernel": single[dom], "algorithmic_bytes_per_launch": bytes_per_launch,
-                    "kernel_ms_per_launch": round(per_call[dom], 4),
-                    "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
-                    "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
-                    "path_frac": round(value * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9
-                                       / HBM_PEAK_GBS, 8),
-                    "ransac_f64": ransac_f64(per_call.get("ransac"), W, H, N, B)}
+        roofline = roofline_of(per_call, value, W, H, N, B, m_avg)
+    # the other schedules of the same workload, on the GPU (never `value`)
+    i_last = args.warmup + args.steps - 1
+    legs = {}
+    if not args.no_ref_equivalent:
+        legs["reference_equivalent"] = ref_equivalent_leg(args, pool, corners, scene.K, ctx, value,
+                                                          recs, (i_last % n_windows) * B)
+    if not args.no_host_fed:
+        for f in fss:
+            f.set_profiling(False)
+        legs["host_fed"] = host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, value)
 
     cpu = None
     pose_check = None
+    pose_check_32 = None
     if args.cpu_seconds > 0:
-        cpu, ref = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds)
+        cpu, ref = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds,
+                                ref_equivalent=not args.no_ref_equivalent)
+        if "reference_equivalent" in legs and cpu.get("reference_equivalent"):
+            re = legs["reference_equivalent"]
+            re["cpu_value"] = cpu["reference_equivalent"]["value"]
+            re["speedup_vs_cpu_same_mode"] = round(re["value"] / max(re["cpu_value"], 1e-9), 1)
         # the same pairs on the GPU (window 0), compared with the oracle's R, t
         fss[0].process(pool[0:B + 1], recs_t[0], wait_torch=False)
         fss[0].sync()
@@ -249,6 +259,8 @@ def main():
         pose_check = {"pairs": n, "bit_identical": ident, "max_abs_R_err": err_r, "max_abs_t_err": err_t,
                       "ate_m": ate, "reference": "oracle/ C++ restatement, same frames; ATE = RMS position "
                                                  "difference of the marker-scaled chained trajectories"}
+        if args.pose_check_32 > 0:
+            pose_check_32 = pose_check_opencv32(pool, scene.K, N, args.max_iters, args.pose_check_32, ctx)
 
     dropin = dropin_rate(pool, corners, scene.K, N, args.dropin_seconds) if args.dropin_seconds > 0 else None
 
@@ -277,9 +289,185 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "pose_check": pose_check,
+        "pose_check_opencv32": pose_check_32,
         "dropin": dropin,
+        "legs": legs,
     }
+    if cpu is not None:
+        out["speedup_vs_cpu_same_mode"] = {"streaming": round(value / max(cpu["value"], 1e-9), 1)}
+        if "reference_equivalent" in legs and "speedup_vs_cpu_same_mode" in legs["reference_equivalent"]:
+            out["speedup_vs_cpu_same_mode"]["reference_equivalent"] = \
+                legs["reference_equivalent"]["speedup_vs_cpu_same_mode"]
+        out["speedup_vs_cpu_same_mode"]["cpu_threads"] = cpu["cores"]
     print(json.dumps(out), flush=True)
+
+
+def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, stream_first_pair):
+    """The reference's own schedule on the GPU: visual_odometry_calculations
+    re-detects BOTH frames of every pair (visual_odometry_v3.py:387-392), so a
+    step of B pairs detects 2B frames (FrameStream.process_pairs /
+    dvo_stream_process_pairs: pair p = frames 2p, 2p+1), then matches, RANSAC,
+    recoverPose and the pose tail as the streaming step.  The paired frame
+    tensors are gathered from the same device pool before timing.  Its
+    records must equal the streaming schedule's byte for byte (detection is
+    a function of the frame), which is checked on the streaming run's last
+    window."""
+    import torch
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    W, H, N, B, S = args.width, args.height, args.nfeatures, args.batch, max(1, args.streams)
+    n_windows = max(1, (len(pool) - 1) // B)
+    dev = pool.device
+    pp = [pool.index_select(0, torch.tensor([w * B + p + j for p in range(B) for j in (0, 1)], device=dev))
+          .contiguous() for w in range(n_windows)]
+    fss = [FrameStream(W, H, K, nfeatures=N, max_frames=2 * B, max_iters=args.max_iters, ctx=ctx) for _ in range(S)]
+    for f in fss[1:]:
+        f.share_pose(fss[0])
+    recs = [f.new_records(B) for f in fss]
+    T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    fss[0].reset_pose()
+    torch.cuda.synchronize()
+
+    def step(i):
+        w, k = i % n_windows, i % S
+        s0 = w * B
+        fss[k].process_pairs(pp[w], recs[k], wait_torch=False)
+        fss[k].pose_tail(corners[s0:s0 + B], corners[s0 + 1:s0 + B + 1], MARKER_LEN, T_rel[k], T_abs[k],
+                         wait_torch=False)
+
+    def sync_all():
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    sync_all()
+    dt = time.perf_counter() - t0
+    # the streaming run's last window through the paired schedule: identical records
+    w = stream_first_pair // B
+    fss[0].process_pairs(pp[w], recs[0], wait_torch=False)
+    fss[0].sync()
+    same = bool(np.array_equal(FrameStream.records_numpy(recs[0], B).view(np.uint8), stream_recs.view(np.uint8)))
+    for f in fss:
+        f.close()
+    del pp, fss, recs
+    torch.cuda.empty_cache()
+    value = B * args.steps / dt
+    return {"value": round(value, 2), "unit": "frames/s", "ms_per_step": round(1e3 * dt / args.steps, 3),
+            "frames_detected_per_step": 2 * B, "pairs_per_step": B, "vs_streaming": round(value / stream_value, 4),
+            "records_identical_to_streaming": same,
+            "schedule": "reference-equivalent: both frames of every pair detected (v3:387-392), 2B detections "
+                        "per B pairs, two batches in flight; value counts pairs (= new frames of the stream)"}
+
+
+def host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, stream_value):
+    """Frames arriving from host memory, as the ROS harness hands them over
+    (trajectory_evaluation_dual_process.py:154-164): the pool is held in
+    pinned host memory, each step's B + 1 frames are copied host-to-device
+    on a copy stream into a ring of device slots (one more slot than batches
+    in flight), and the library stream waits for the copy's event, so the
+    H2D copy of step i+1 overlaps the compute of step i.  The link rate is
+    the same copies timed alone.  Never `value`."""
+    import torch
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    B, S = args.batch, len(fss)
+    R = S + 1
+    hpool = torch.empty(pool.shape, dtype=pool.dtype, pin_memory=True)
+    hpool.copy_(pool)
+    slots = [torch.empty((B + 1,) + tuple(pool.shape[1:]), dtype=pool.dtype, device=pool.device) for _ in range(R)]
+    cs = torch.cuda.Stream(device=pool.device)
+    used = [None] * R
+    torch.cuda.synchronize()
+
+    def step(i):
+        s0, k, r = (i % n_windows) * B, i % S, i % R
+        with torch.cuda.stream(cs):
+            if used[r] is not None:
+                cs.wait_event(used[r])  # the compute that last read this slot has finished
+            slots[r].copy_(hpool[s0:s0 + B + 1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        fs = fss[k]
+        fs.wait_event(ev)
+        fs.process(slots[r], recs_t[k], wait_torch=False)
+        fs.pose_tail(corners[s0:s0 + B], corners[s0 + 1:s0 + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
+        used[r] = fs.record_event()
+
+    def sync_all():
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    sync_all()
+    dt = time.perf_counter() - t0
+    # the link alone: the same copies back to back on the copy stream
+    nb = slots[0].numel()
+    reps = max(3, min(args.steps, 10))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    with torch.cuda.stream(cs):
+        for i in range(reps):
+            s0 = (i % n_windows) * B
+            slots[i % R].copy_(hpool[s0:s0 + B + 1], non_blocking=True)
+    cs.synchronize()
+    dl = time.perf_counter() - t1
+    link = nb * reps / dl / 1e9
+    value = B * args.steps / dt
+    del slots, hpool
+    torch.cuda.empty_cache()
+    return {"value": round(value, 2), "unit": "frames/s", "ms_per_step": round(1e3 * dt / args.steps, 3),
+            "h2d_bytes_per_step": nb, "h2d_link_GBps": round(link, 2),
+            "link_bound_frames_per_s": round(link * 1e9 / (nb / (B + 1)) * B / (B + 1), 1),
+            "vs_device_resident": round(value / stream_value, 4),
+            "schedule": "pinned host frames, async H2D on a copy stream into a ring of S+1 device slots "
+                        "overlapped with compute; B+1 frames copied per B-pair step"}
+
+
+def pose_check_opencv32(pool, K, nfeatures, max_iters, n_pairs, ctx):
+    """OpenCV 3.2 semantics (FrameStream(opencv="3.2"): INTER_LINEAR pyramid,
+    3.2 retainBest, 3.x reverse-pass cross check) on the first n_pairs of the
+    same stream, against the oracle in the same mode (streaming, features
+    reused)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from droplet_visual_odometry_amd.stream import FrameStream
+    W, H = pool.shape[2], pool.shape[1]
+    n = min(n_pairs, len(pool) - 1)
+    fs = FrameStream(W, H, K, nfeatures=nfeatures, max_frames=n + 1, max_iters=max_iters, ctx=ctx, opencv="3.2")
+    rec = fs.process(pool[0:n + 1])
+    fs.sync()
+    g = FrameStream.records_numpy(rec, n)
+    fs.close()
+    host = lambda i: pool[i].cpu().numpy()  # noqa: E731
+    kp = oracle.detect_and_compute(host(0), nfeatures, semantics=oracle.OCV32)
+    ident = 0
+    for i in range(n):
+        r = oracle.pair_pose(host(i), host(i + 1), K, nfeatures, max_iters=max_iters, kp_prev=kp,
+                             semantics=oracle.OCV32)
+        kp = (r["kp_cur"], r["desc_cur"])
+        if r["R"] is None:
+            ident += int(g["status"][i] != 0)
+            continue
+        ident += int(g["status"][i] == 0 and g["n_matches"][i] == len(r["q"])
+                     and np.array_equal(g["R"][i].reshape(3, 3), r["R"])
+                     and np.array_equal(g["t"][i], r["t_unit"].ravel()))
+    del torch
+    return {"pairs": n, "bit_identical": ident,
+            "reference": "oracle/ in OpenCV 3.2 mode (INTER_LINEAR pyramid, 3.2 retainBest, 3.x cross check), "
+                         "same frames, streaming"}
 
 
 def main_sharded(args, world, rank, local_rank, backend, dev, scene):
@@ -318,7 +506,7 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
 
     def step(i):
         j = i % n_windows
-        return run.step(pools[j], corners[j][:-1], corners[j][1:])[0]
+        return run.step(pools[j], corners[j][:-1], corners[j][1:], wait_torch=False)[0]  # frames resident
 
     sync_all = run.sync
     for i in range(args.warmup):
@@ -393,46 +581,71 @@ def chained_ate(fs, pool, corners, K, ref, B):
     return float(np.sqrt(np.mean(err))) if err else None
 
 
-def pmc_counts(kernel, W, H, N, B):
-    """Per-launch PMC figures of `kernel` from the committed round profile
-    (profiles/PMC_TRAFFIC, tools/profile_round.sh): HBM bytes (FETCH_SIZE +
-    WRITE_SIZE, corrected by the known-bytes calibration of the kernel's access
-    widths) and SQ_INSTS_VALU, scaled per frame from the profiled batch to a
-    launch over B + 1 frames.  PMC counters cannot run inside the timed loop."""
-    path = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
-    try:
-        doc = json.load(open(path))
-    except (OSError, ValueError):
+def pmc_doc(pattern, W, H, N):
+    """(path, document) of the newest committed PMC document under profiles/
+    (round tags sort by name) collected on this workload, or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+        try:
+            doc = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        c = doc.get("config", {}) if isinstance(doc, dict) else {}
+        if (c.get("width"), c.get("height"), c.get("nfeatures")) == (W, H, N) and c.get("batch") \
+                and isinstance(doc.get("kernels"), dict):
+            best = (path, doc)
+    return best
+
+
+def kernels_of(stage, names):
+    """The profiled kernel names (rocprofv3 spells templates "void k<...>") of a stage."""
+    out = []
+    for name in names:
+        base = name.replace("void ", "").split("<")[0].strip()
+        if any(base == k or (k.endswith("_") and base.startswith(k)) for k in STAGE_KERNELS[stage]):
+            out.append(name)
+    return sorted(out)
+
+
+def pmc_counts(stage, W, H, N, B):
+    """Per-launch PMC figures of a stage's kernels from the committed round
+    profile (tools/profile_round.sh): HBM bytes (fetched bytes from the
+    read-request-size counters, calibrated against kernels of known traffic,
+    plus WRITE_SIZE) and SQ_INSTS_VALU, scaled from the profiled batch to a
+    launch over this run's units (B + 1 frames, or B pairs).  PMC counters
+    cannot run inside the timed loop."""
+    found = pmc_doc(PMC_TRAFFIC_GLOB, W, H, N)
+    if found is None:
         return None
-    c = doc.get("config", {})
-    k = doc.get("kernels", {}).get(kernel)
-    if k is None or (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
+    path, doc = found
+    c = doc["config"]
+    ks = kernels_of(stage, doc["kernels"])
+    if not ks:
         return None
-    scale = (B + 1) / (c["batch"] + 1)
-    src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc passes at batch {c['batch']}"
-    src += ")" if c["batch"] == B else f", scaled per frame to batch {B})"
-    return {"traffic": round((k["fetch_bytes"] + k["write_bytes"]) * scale),
-            "traffic_raw": round((k["fetch_bytes_raw"] + k["write_bytes_raw"]) * scale),
-            "calibrated": bool(k.get("calibrated")), "widths": k.get("widths"),
-            "valu_insts": k.get("SQ_INSTS_VALU", 0.0) * scale, "source": src}
+    scale = B / c["batch"] if stage in PAIR_STAGES else (B + 1) / (c["batch"] + 1)
+    tot = lambda key: sum(doc["kernels"][k].get(key, 0.0) for k in ks)  # noqa: E731
+    src = f"profiles/{os.path.basename(path)} (rocprofv3 --pmc passes at batch {c['batch']}"
+    src += ")" if c["batch"] == B else f", scaled per unit to batch {B})"
+    return {"traffic": round((tot("fetch_bytes") + tot("write_bytes")) * scale),
+            "traffic_raw": round((tot("fetch_bytes_raw") + tot("write_bytes_raw")) * scale),
+            "calibrated": all(bool(doc["kernels"][k].get("calibrated")) for k in ks),
+            "valu_insts": tot("SQ_INSTS_VALU") * scale, "kernels": ks, "source": src}
 
 
 def ransac_f64(ms_per_launch, W, H, N, B):
     """f64 issue fraction of the RANSAC kernel group (sampling, stage A, Durand-Kerner, stage C, score,
-    replay, finish): its f64 VALU FLOPs per launch (profiles/PMC_F64: SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64,
-    FMA = 2 FLOP, a wave64 instruction = 64 lanes; scaled per pair from the profiled batch) / the group's
-    HIP-event time on the library stream / the FP64 vector peak.  The event time includes the waits for the
-    other stream's kernels sharing the CUs, so this is the rate the stage achieves in the pipeline."""
+    replay, finish): its f64 VALU FLOPs per launch (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, FMA = 2 FLOP, a
+    wave64 instruction = 64 lanes; scaled per pair from the profiled batch) / the group's HIP-event time on
+    the library stream / the FP64 vector peak.  The event time includes the waits for the other stream's
+    kernels sharing the CUs, so this is the rate the stage achieves in the pipeline."""
     if not ms_per_launch:
         return None
-    path = os.path.join(ROOT, "profiles", PMC_F64)
-    try:
-        doc = json.load(open(path))
-    except (OSError, ValueError):
+    found = pmc_doc(PMC_F64_GLOB, W, H, N)
+    if found is None:
         return None
-    c = doc.get("config", {})
-    if (c.get("width"), c.get("height"), c.get("nfeatures")) != (W, H, N) or not c.get("batch"):
-        return None
+    path, doc = found
+    c = doc["config"]
     scale = B / c["batch"]
     ks = {k: v for k, v in doc["kernels"].items() if "ransac_" in k}  # incl. "void ransac_score_kernel<16>"
     flops = sum(v["f64_flops_full_wave"] for v in ks.values()) * scale
@@ -440,11 +653,70 @@ def ransac_f64(ms_per_launch, W, H, N, B):
     achieved = flops / (ms_per_launch * 1e-3) / 1e12
     # issue view: a wave64 f64 instruction holds a SIMD's f64 pipe 4 cycles (16 lanes per cycle)
     issue = insts * 4 / (ms_per_launch * 1e-3 * 1024 * 2.4e9)
+    per_kernel = {k: round(v["f64_wave_insts"] * scale) for k, v in sorted(ks.items())}
     return {"bound": "f64 valu", "achieved": round(achieved, 3), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / F64_PEAK_TFLOPS, 5), "issue_frac": round(issue, 5),
-            "f64_wave_insts_per_launch": round(insts),
+            "f64_wave_insts_per_launch": round(insts), "f64_wave_insts_per_kernel": per_kernel,
             "f64_flops_per_launch": round(flops), "ms_per_launch": round(ms_per_launch, 4),
-            "kernels": sorted(ks), "source": f"profiles/{PMC_F64} (batch {c['batch']}, scaled per pair to {B})"}
+            "kernels": sorted(ks), "source": f"profiles/{os.path.basename(path)} (batch {c['batch']}, scaled per "
+                                             f"pair to {B})"}
+
+
+def hbm_roofline(stage, ms, W, H, N, B, m_avg):
+    """A stage priced against HBM: its algorithmic bytes per launch (stage_bytes x units) / its HIP-event time."""
+    sb = stage_bytes(W, H, N, m_avg)
+    units = B if stage in PAIR_STAGES else B + 1
+    bytes_per_launch = sb[stage] * units
+    achieved = bytes_per_launch / (ms * 1e-3) / 1e9
+    pmc = pmc_counts(stage, W, H, N, B)
+    valu = None
+    if pmc and pmc["valu_insts"]:
+        va = pmc["valu_insts"] / (ms * 1e-3)
+        valu = {"achieved": round(va / 1e9, 3), "peak": VALU_PEAK_WIPS / 1e9, "unit": "G wave-instructions/s",
+                "frac": round(va / VALU_PEAK_WIPS, 6), "insts_per_launch": round(pmc["valu_insts"]),
+                "note": "SQ_INSTS_VALU per launch / the launch's HIP-event time; peak = one wave64 VALU "
+                        "instruction per 2 cycles per SIMD x 1024 SIMDs x 2.4 GHz (MI355X_MICROARCH.md)"}
+    return {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6),
+            "traffic": pmc["traffic"] if pmc else None,
+            "traffic_raw": pmc["traffic_raw"] if pmc else None,
+            "traffic_calibrated": pmc["calibrated"] if pmc else None,
+            "traffic_source": pmc["source"] if pmc else None,
+            "valu": valu, "valu_frac": valu["frac"] if valu else None,
+            "stage": stage, "kernel": ", ".join(pmc["kernels"]) if pmc else " / ".join(STAGE_KERNELS[stage]),
+            "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms_per_launch": round(ms, 4)}
+
+
+def roofline_of(per_call, value, W, H, N, B, m_avg):
+    """The roofline of the dominant stage: the HIP-event stage with the most
+    device time per step, whatever its bound.  The RANSAC group (scalar f64
+    solver and scorer) is priced against the FP64 vector peak, every other
+    stage against HBM with its algorithmic bytes.  The
+    longest single-kernel HBM stage is reported beside it (`hbm_dominant`),
+    and the f64 view of the RANSAC group always (`ransac_f64`)."""
+    from droplet_visual_odometry_amd.plan import algorithmic_bytes_per_frame
+    dom = max(per_call, key=lambda k: per_call.get(k, 0.0))
+    rf = ransac_f64(per_call.get("ransac"), W, H, N, B)
+    single = [k for k in ("fast", "blur", "describe") if per_call.get(k)]
+    hdom = max(single, key=lambda k: per_call[k]) if single else None
+    hbm_dom = hbm_roofline(hdom, per_call[hdom], W, H, N, B, m_avg) if hdom else None
+    if dom == "ransac" and rf is not None:
+        pmc = pmc_counts("ransac", W, H, N, B)
+        roof = {"bound": "f64", "achieved": rf["achieved"], "peak": rf["peak"], "unit": "TFLOP/s",
+                "frac": rf["frac"], "traffic": pmc["traffic"] if pmc else None,
+                "traffic_source": pmc["source"] if pmc else None, "stage": "ransac",
+                "kernel": "RANSAC group: " + ", ".join(rf["kernels"]), "kernel_ms_per_launch": rf["ms_per_launch"],
+                "note": "dominant stage = most HIP-event time per step; the RANSAC group is scalar f64 work "
+                        "(5-point solve, Durand-Kerner, Sampson scoring), priced against the 78.6 TFLOP/s FP64 "
+                        "vector peak; issue_frac in ransac_f64"}
+    else:
+        roof = hbm_roofline(dom, per_call[dom], W, H, N, B, m_avg) if dom != "ransac" else dict(hbm_dom or {})
+    roof.update({"dominant_stage": dom,
+                 "stage_ms_per_step": {k: round(v, 4) for k, v in per_call.items()},
+                 "path_algorithmic_bytes_per_frame": algorithmic_bytes_per_frame(W, H, N, m_avg),
+                 "path_frac": round(value * algorithmic_bytes_per_frame(W, H, N, m_avg) / 1e9 / HBM_PEAK_GBS, 8),
+                 "hbm_dominant": hbm_dom, "ransac_f64": rf})
+    return roof
 
 
 def dropin_rate(pool, corners, K, nfeatures, seconds, n_frames=48):
@@ -502,7 +774,7 @@ def cpu_threads():
     return max(1, n)
 
 
-def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
+def cpu_baseline(pool, K, nfeatures, max_iters, seconds, ref_equivalent=False):
     """The oracle (restated OpenCV path, C++ built -O3 -march=native for this
     host) on the same stream, in streaming mode (each frame detected once,
     its features reused by the next pair):
@@ -510,8 +782,11 @@ def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
                     (trajectory_evaluation_dual_process.py:172);
       all cores     the stream split into contiguous runs, one per thread
                     (ctypes releases the GIL inside the C++ calls), each run
-                    sequential with feature reuse -- SURVEY.md §8d (2).
-    Each leg runs about `seconds`.  value = the all-cores figure."""
+                    sequential with feature reuse -- SURVEY.md §8d (2);
+      reference-equivalent (ref_equivalent)  all cores again, but every pair
+                    detects both of its frames, as visual_odometry_calculations
+                    does (visual_odometry_v3.py:387-392).
+    Each leg runs about `seconds`.  value = the all-cores streaming figure."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
@@ -536,27 +811,36 @@ def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
     done = [0] * T
     deadline = time.perf_counter() + seconds
 
-    def worker(t):
+    def worker(t, reuse):
         a = t * run
         if a + 1 >= len(pool):
             return
-        kp = oracle.detect_and_compute(host(a), nfeatures)
+        kp = oracle.detect_and_compute(host(a), nfeatures) if reuse else None
         j = a
         while j + 1 < min(len(pool), a + run + 1) and time.perf_counter() < deadline:
             r = oracle.pair_pose(host(j), host(j + 1), K, nfeatures, max_iters=max_iters, kp_prev=kp)
-            kp = (r["kp_cur"], r["desc_cur"])
+            kp = (r["kp_cur"], r["desc_cur"]) if reuse else None
             done[t] += 1
             j += 1
 
-    t1 = time.perf_counter()
-    ths = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    dtn = time.perf_counter() - t1
-    nn = sum(done)
+    def all_threads(reuse):
+        t1 = time.perf_counter()
+        ths = [threading.Thread(target=worker, args=(t, reuse)) for t in range(T)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return sum(done), time.perf_counter() - t1
+
+    nn, dtn = all_threads(True)
     W, H = pool.shape[2], pool.shape[1]
+    re = None
+    if ref_equivalent:
+        done[:] = [0] * T
+        deadline = time.perf_counter() + seconds
+        nr, dtr = all_threads(False)
+        re = {"value": round(nr / dtr, 3), "cores": T,
+              "sample": f"{nr} pairs in {dtr:.1f} s on {T} threads, both frames of every pair detected (v3:387-392)"}
     return ({"value": round(nn / dtn, 3), "unit": "frames/s", "cores": T, "kind": "port",
              "sample": f"{nn} pairs of the same {W}x{H} stream in {dtn:.1f} s on {T} threads (the stream split into "
                        f"{T} contiguous runs, each sequential with feature reuse; each run's first detect included); "
@@ -564,6 +848,7 @@ def cpu_baseline(pool, K, nfeatures, max_iters, seconds):
                        f"({os.path.basename(lib_path)})",
              "single_core": {"value": round(n1 / dt1, 3), "cores": 1,
                              "sample": f"{n1} consecutive pairs in {dt1:.1f} s, first frame's detect included"},
+             "reference_equivalent": re,
              "host_cpus": os.cpu_count(), "cpu_model": model}, ref)
 
 

@@ -64,6 +64,7 @@ struct dvo_stream {
     dvo_stream* carry_owner = nullptr;  // stream whose carry this one uses (itself by default)
     bool own_hs = false;
     int last_nframes = 0;
+    int last_pairs = 0;           // pairs of that call (n - 1 for a stream, n / 2 for independent pairs)
     bool last_has_pairs = false;  // the last call ran match + geometry
     const dvo_pair_record* last_rec = nullptr;  // the caller's records of that call (read by the pose tail)
     const uint8_t* last_frames = nullptr;       // the frames of that call (get_pyramid recomputes blurred levels)
@@ -362,6 +363,7 @@ StreamParams params_of(dvo_stream* s, const uint8_t* frames, int nframes, int64_
     P.frame_stride = frame_stride;
     P.in_pitch = pitch;
     P.nframes = nframes;
+    P.pair_step = 1;
     return P;
 }
 
@@ -502,11 +504,13 @@ int collect_events(dvo_stream* s) {
 }
 
 int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, int pitch, dvo_pair_record* d_rec,
-               bool detect_only) {
+               bool detect_only, int pair_step = 1) {
     dvo_ctx* ctx = s->ctx;
     StreamParams P = params_of(s, d_frames, n, fstride, pitch);
+    P.pair_step = pair_step;
+    const int pairs = stream_pairs(P);
     hipEvent_t* ev = nullptr;
-    if (s->profiling && !detect_only && n >= 2) {
+    if (s->profiling && !detect_only && pairs >= 1) {
         int rc = acquire_events(s, &ev);
         if (rc) return rc;
     }
@@ -516,7 +520,8 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     s->last_frames = d_frames;
     s->last_fstride = fstride;
     s->last_pitch = pitch;
-    s->last_has_pairs = !detect_only && n >= 2;
+    s->last_has_pairs = !detect_only && pairs >= 1;
+    s->last_pairs = s->last_has_pairs ? pairs : 0;
     s->last_rec = d_rec;
     if (!s->last_has_pairs) return DVO_OK;
     HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, ev));
@@ -654,7 +659,7 @@ int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const doub
     if (k < 2 || !d_corners_prev || !d_corners_cur || !d_T_rel || !d_T_abs)
         return fail(ctx, DVO_EINVAL, "pose tail needs >= 2 corners per frame and output buffers");
     if (!s->last_has_pairs) return fail(ctx, DVO_EINVAL, "pose tail needs a preceding dvo_stream_process");
-    const int pairs = s->last_nframes - 1;
+    const int pairs = s->last_pairs;
     HIP_TRY(hipSetDevice(ctx->device));
     hipEvent_t* ev = (s->profiling && !s->ev_pending.empty()) ? s->ev_pending.back().data() : nullptr;
     dvo_stream* o = s->carry_owner;  // pose tails on one carry run in call order, across streams
@@ -713,13 +718,10 @@ int dvo_stream_stage_times(dvo_stream* s, double* ms, int* calls) {
 
 void* dvo_stream_hip_stream(dvo_stream* s) { return s ? (void*)s->hs : nullptr; }
 
-int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
-                       dvo_pair_record* d_records) {
-    if (!s) return DVO_EINVAL;
+static int process_frames(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                   dvo_pair_record* d_records, int pair_step) {
     dvo_ctx* ctx = s->ctx;
-    if (n_frames < 1 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range");
     if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
-    if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
     HIP_TRY(hipSetDevice(ctx->device));
     if (((uintptr_t)d_frames | (uintptr_t)frame_stride | (uintptr_t)stride) & 3) {
         // the byte kernels read level 0 in 4-byte words: realign into the slab
@@ -727,9 +729,27 @@ int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int
         for (int i = 0; i < n_frames; ++i)
             HIP_TRY(hipMemcpy2DAsync(s->d_frames + (size_t)i * pw * s->cfg.height, pw, d_frames + i * frame_stride,
                                      stride, s->cfg.width, s->cfg.height, hipMemcpyDeviceToDevice, s->hs));
-        return run_stream(s, s->d_frames, n_frames, (int64_t)pw * s->cfg.height, pw, d_records, false);
+        return run_stream(s, s->d_frames, n_frames, (int64_t)pw * s->cfg.height, pw, d_records, false, pair_step);
     }
-    return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false);
+    return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false, pair_step);
+}
+
+int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                       dvo_pair_record* d_records) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (n_frames < 1 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range");
+    if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
+    return process_frames(s, d_frames, n_frames, frame_stride, stride, d_records, 1);
+}
+
+int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
+                             dvo_pair_record* d_records) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (n_pairs < 1 || 2 * (int64_t)n_pairs > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_pairs out of range");
+    if (!d_records) return fail(ctx, DVO_EINVAL, "null records");
+    return process_frames(s, d_frames, 2 * n_pairs, frame_stride, stride, d_records, 2);
 }
 
 int dvo_stream_sync(dvo_stream* s) {
@@ -765,7 +785,7 @@ int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t
 int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m) {
     if (!s || !m) return DVO_EINVAL;
     dvo_ctx* ctx = s->ctx;
-    if (pair < 0 || pair >= s->last_nframes - 1) return fail(ctx, DVO_EINVAL, "pair out of range");
+    if (pair < 0 || pair >= s->last_pairs) return fail(ctx, DVO_EINVAL, "pair out of range");
     HIP_TRY(hipStreamSynchronize(s->hs));
     int nm = 0;
     HIP_TRY(hipMemcpy(&nm, s->buf.nmatch + pair, sizeof(int), hipMemcpyDeviceToHost));

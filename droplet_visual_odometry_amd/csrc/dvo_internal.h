@@ -152,7 +152,16 @@ struct StreamParams {   // passed by value to every batch kernel
     int64_t frame_stride;
     int in_pitch;
     int nframes;
+    // Pair layout: 1 = a stream (pair p is frames p, p+1: each frame detected once and shared by two
+    // pairs); 2 = independent pairs (pair p is frames 2p, 2p+1), the reference's own schedule, which
+    // detects both frames of every pair (visual_odometry_v3.py:387-392).
+    int pair_step;
 };
+
+__host__ __device__ inline int stream_pairs(const StreamParams& P) {
+    return P.pair_step == 2 ? P.nframes / 2 : P.nframes - 1;
+}
+__host__ __device__ inline int pair_frame(const StreamParams& P, int p) { return P.pair_step == 2 ? 2 * p : p; }
 
 __host__ __device__ inline const uint8_t* level_ptr(const StreamParams& P, int f, int l) {
     return l == 0 ? P.frames + (int64_t)f * P.frame_stride : P.buf.pyr + (int64_t)f * P.plan.pyr_stride + P.plan.L[l].pyr_off;

@@ -1553,7 +1553,7 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     __shared__ int s_moff[HYPS * 10];      // the model's offset in g.models (the f64 test)
 #endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
-    static_assert(HYPS <= 64, "one wave prefixes the model counts");
+    static_assert(HYPS < 64, "one wave prefixes the model counts; lane hn (< 64) writes the total");
     if (tid < 64) {  // model counts of the block's hypotheses: one load each, a wave prefix sum
         const int c = tid < hn ? g.nmod[hbase + tid] : 0;
         int x = c;
@@ -2034,7 +2034,8 @@ __global__ void triangulate_kernel(const double* P, const double* x, int k, doub
 
 __global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec) {
     const int p = blockIdx.x * 64 + threadIdx.x;
-    if (p >= P.nframes - 1) return;
+    if (p >= stream_pairs(P)) return;
+    const int fp = pair_frame(P, p);  // the pair's frames are fp, fp + 1
     dvo_pair_record r;
     const int32_t* info = g.info + (int64_t)p * 4;
     const double* E = g.E + (int64_t)p * 90;
@@ -2043,16 +2044,16 @@ __global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec)
     for (int k = 0; k < 9; ++k) r.R[k] = ok ? Rt[k] : 0.0;
     for (int k = 0; k < 3; ++k) r.t[k] = ok ? Rt[9 + k] : 0.0;
     for (int k = 0; k < 9; ++k) r.E[k] = info[0] >= 3 ? E[k] : 0.0;
-    r.n_kp_prev = P.buf.nkp[p];
-    r.n_kp_cur = P.buf.nkp[p + 1];
+    r.n_kp_prev = P.buf.nkp[fp];
+    r.n_kp_cur = P.buf.nkp[fp + 1];
     r.n_matches = P.buf.nmatch[p];
     r.n_inliers = info[1];
     r.n_good = ok ? g.good[p] : 0;
     r.ransac_iters = info[2];
     // ECAP (a buffer overflowed) > ENOFEAT (an empty frame: the reference's
     // bf.match(None, ...) raises, v3:219) > the RANSAC / pose status.
-    r.status = (P.buf.status[p] | P.buf.status[p + 1])         ? DVO_ECAP
-               : (P.buf.nkp[p] == 0 || P.buf.nkp[p + 1] == 0) ? DVO_ENOFEAT
+    r.status = (P.buf.status[fp] | P.buf.status[fp + 1])         ? DVO_ECAP
+               : (P.buf.nkp[fp] == 0 || P.buf.nkp[fp + 1] == 0) ? DVO_ENOFEAT
                                                               : info[3];
     r.n_models = info[0] / 3;
     r.n_hypotheses = g.rs[p].h1;  // hypotheses [0, h1) were sampled and solved
@@ -2279,7 +2280,7 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
 
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
                            hipEvent_t* ev) {
-    const int pairs = P.nframes - 1;
+    const int pairs = stream_pairs(P);
     if (pairs <= 0) return hipSuccess;
     mark(ev, 6, 0, s);
     hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac, s);

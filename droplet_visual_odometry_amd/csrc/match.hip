@@ -197,14 +197,15 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
     const int p = L / nqb, qb = L - p * nqb;
     if (p >= pairs) return;
     const int cap = P.plan.kp_cap;
-    const int nq = O.nq_fix >= 0 ? O.nq_fix : min(P.buf.nkp[p], cap);
-    const int nt = O.nt_fix >= 0 ? O.nt_fix : min(P.buf.nkp[p + 1], cap);
+    const int fp = pair_frame(P, p);  // the pair's previous frame; its current frame is fp + 1
+    const int nq = O.nq_fix >= 0 ? O.nq_fix : min(P.buf.nkp[fp], cap);
+    const int nt = O.nt_fix >= 0 ? O.nt_fix : min(P.buf.nkp[fp + 1], cap);
     const int qbase = qb * kMQB;
     if (qbase >= nq) return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const uint4* XQ = reinterpret_cast<const uint4*>(O.q0 + p * O.stride);
-    const uint2* XT = reinterpret_cast<const uint2*>(O.t0 + p * O.stride);
+    const uint4* XQ = reinterpret_cast<const uint4*>(O.q0 + fp * O.stride);
+    const uint2* XT = reinterpret_cast<const uint2*>(O.t0 + fp * O.stride);
     int32_t* fwd = P.buf.nn + (int64_t)p * cap;
     int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
     const int qs = qbase + wid * 64;  // this wave's first query
@@ -356,12 +357,13 @@ __global__ __launch_bounds__(kXNT) void crosscheck_stream_kernel(StreamParams P,
     __shared__ int scan_lds[32];
     const int p = blockIdx.x;
     const int cap = P.plan.kp_cap;
-    const int nq = min(P.buf.nkp[p], cap), nt = min(P.buf.nkp[p + 1], cap);
+    const int fp = pair_frame(P, p);
+    const int nq = min(P.buf.nkp[fp], cap), nt = min(P.buf.nkp[fp + 1], cap);
     const int32_t* fwd = P.buf.nn + (int64_t)p * cap;
     const int32_t* bwd = P.buf.nn + ((int64_t)P.nframes + p) * cap;
     const int m = crosscheck_sort(fwd, bwd, nq, nt, mode, keys, scan_lds);
-    const dvo_keypoint* ka = P.buf.kps + (int64_t)p * cap;
-    const dvo_keypoint* kb = P.buf.kps + (int64_t)(p + 1) * cap;
+    const dvo_keypoint* ka = P.buf.kps + (int64_t)fp * cap;
+    const dvo_keypoint* kb = P.buf.kps + (int64_t)(fp + 1) * cap;
     int32_t* mq = P.buf.mq + (int64_t)p * cap;
     int32_t* mt = P.buf.mt + (int64_t)p * cap;
     float* md = P.buf.md + (int64_t)p * cap;
@@ -444,17 +446,18 @@ __global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* fw
 }  // namespace
 
 hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev) {
-    if (P.nframes < 2) return hipSuccess;
+    const int pairs = stream_pairs(P);
+    if (pairs < 1) return hipSuccess;
     mark(ev, 5, 0, s);
     const int cap = P.plan.kp_cap;
     // backward keys start at 0x7F7F7F7F ("none") and are lowered by atomicMin
     hipError_t e = hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F, sizeof(int32_t) * (size_t)P.nframes * cap, s);
     if (e != hipSuccess) return e;
-    const int pairs = P.nframes - 1, nqb = (cap + kMQB - 1) / kMQB;
+    const int nqb = (cap + kMQB - 1) / kMQB;
     const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
     const NnOperands O{P.buf.desc, P.buf.desc + (int64_t)cap * 32, (int64_t)cap * 32, -1, -1};
     hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, O, pairs, nqb, 1);
-    hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(P.nframes - 1), dim3(kXNT), 0, s, P, cross_check);
+    hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(pairs), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();
 }
@@ -476,6 +479,7 @@ hipError_t launch_match_pair(const uint8_t* d_q, int nq, const uint8_t* d_t, int
     StreamParams P{};
     P.plan.kp_cap = cap;
     P.nframes = 2;
+    P.pair_step = 1;
     P.buf.nn = static_cast<int32_t*>(d_work);
     int32_t* fwd = P.buf.nn;
     int32_t* bwd = P.buf.nn + 2 * (size_t)cap;

@@ -334,9 +334,18 @@ class FlannBasedMatcher:
     restates it).  The trees come from cv::theRNG(), carried per thread across
     calls as in OpenCV.  DMatch.distance is sqrt(float32) of FLANN's squared
     L2 distance, as FlannBasedMatcher::convertToDMatches does for float
-    descriptors, so the 0.75 ratio test (v3:227) compares distances."""
+    descriptors, so the 0.75 ratio test (v3:227) compares distances.
+
+    OpenCV 4.x only: the FLANN bundled with OpenCV 3.2 drew its trees from
+    std::rand / std::random_shuffle, which are not restated, so with
+    OPENCV_SEMANTICS == "3.2" the constructor raises cv.error rather than
+    silently building 4.x trees.  Parity is against oracle/flann.cpp (the
+    restatement); against OpenCV's FLANN itself it is unpinned (no cv2 here)."""
 
     def __init__(self, indexParams=None, searchParams=None):
+        if opencv_semantics(OPENCV_SEMANTICS) == 1:
+            raise error("FlannBasedMatcher reproduces OpenCV 4.x's FLANN (cv::theRNG trees); the OpenCV 3.2 "
+                        "FLANN (std::rand trees) is not implemented -- unset DVO_OPENCV_SEMANTICS=3.2 for flann mode")
         self.indexParams = dict(indexParams or {})
         self.searchParams = dict(searchParams or {})
         if self.indexParams.get("algorithm", 1) != 1:

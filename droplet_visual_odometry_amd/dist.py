@@ -177,15 +177,20 @@ class ShardedStreamRunner:
             if rank == 0 else None
         self.i = 0
 
-    def step(self, frames, c_prev, c_cur):
+    def step(self, frames, c_prev, c_cur, wait_torch: bool = True):
+        """wait_torch (default): order the library stream after work queued on
+        torch's current stream -- the frames' producer and, on a slot's first
+        use, the zero-fill of its send buffer.  Pass False only for frames that
+        are already resident (the slot's first use is still ordered)."""
         import torch
         k = self.i % self.S
+        first_use = self.i < self.S
         self.i += 1
         fs, sh = self.fss[k], self.shs[k]
         if frames.shape[0] != self.n_local + 1:
             raise ValueError(f"rank {self.rank} needs {self.n_local + 1} frames per window")
         fs.wait_event(sh.done)  # the slot's previous collective has read its send buffer
-        fs.process(frames, sh.records, wait_torch=False)
+        fs.process(frames, sh.records, wait_torch=wait_torch or first_use)
         if self.host_gather:
             fs.sync()
         else:

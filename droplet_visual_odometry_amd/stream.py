@@ -47,6 +47,11 @@ class FrameStream:
         self.h = h
         self._ext = torch.cuda.ExternalStream(self.hip_stream, device=self.device)
         self._held = collections.deque()  # (event, tensors) in flight on the library's stream
+        # The last process() call's frames and records: the library keeps raw pointers to both
+        # (dvo_stream_pose_tail reads the records, get_pyramid(blurred) re-reads level 0 of the
+        # frames), so they stay referenced until the next process() or close(), whatever the
+        # caller keeps and whether or not sync() has drained _held.
+        self._last = ()
         self.width, self.height, self.max_frames, self.nfeatures = width, height, max_frames, nfeatures
         self.K = K.reshape(3, 3)
 
@@ -81,6 +86,33 @@ class FrameStream:
         else:
             self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
                                                            frames.stride(1), records.data_ptr() if n > 1 else None))
+        self._last = (frames, records)
+        self._hold(frames, records)
+        return records
+
+    def process_pairs(self, frames: torch.Tensor, records: torch.Tensor | None = None,
+                      wait_torch: bool = True) -> torch.Tensor:
+        """The reference's schedule (dvo_stream_process_pairs): frames holds 2n
+        frames and pair p is frames 2p, 2p+1, each detected on its own, as
+        visual_odometry_calculations re-detects both frames of every pair
+        (visual_odometry_v3.py:387-392).  Records / pose tail as process()."""
+        if frames.dtype != torch.uint8 or frames.dim() != 3 or not frames.is_cuda:
+            raise ValueError("frames must be a uint8 [2n, H, W] device tensor")
+        n2, h, w = frames.shape
+        if (h, w) != (self.height, self.width):
+            raise ValueError(f"frame size {w}x{h} != stream {self.width}x{self.height}")
+        if n2 % 2 or n2 == 0:
+            raise ValueError("frames must hold an even, non-zero number of frames (pairs 2p, 2p+1)")
+        if frames.stride(2) != 1 or frames.stride(1) < w:
+            raise ValueError("frames rows must be contiguous")
+        if records is None:
+            records = self.new_records(n2 // 2)
+            wait_torch = True
+        if wait_torch:
+            self._after_torch()
+        self.ctx.check(self.ctx.lib.dvo_stream_process_pairs(self.h, frames.data_ptr(), n2 // 2, frames.stride(0),
+                                                             frames.stride(1), records.data_ptr()))
+        self._last = (frames, records)
         self._hold(frames, records)
         return records
 
@@ -143,7 +175,7 @@ class FrameStream:
             self._after_torch()
         self.ctx.check(self.ctx.lib.dvo_stream_pose_tail(self.h, corners_prev.data_ptr(), corners_cur.data_ptr(), k,
                                                          float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
-        self._hold(corners_prev, corners_cur, T_rel, T_abs)
+        self._hold(corners_prev, corners_cur, T_rel, T_abs, *self._last)
         return T_rel, T_abs
 
     def set_profiling(self, enable: bool = True):
@@ -194,6 +226,7 @@ class FrameStream:
             self.h = None
             if getattr(self, "_held", None):
                 self._held.clear()
+            self._last = ()
 
     def __del__(self):
         try:

@@ -220,6 +220,16 @@ void dvo_stream_destroy(dvo_stream* s);
 int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
                        dvo_pair_record* d_records);
 int dvo_stream_sync(dvo_stream* s);
+/* The reference's own schedule: visual_odometry_calculations (v3:384-408) runs
+ * compute_current_image_elements on BOTH frames of every pair (v3:387-392), so
+ * each frame is detected twice in a stream.  d_frames holds 2 n_pairs frames;
+ * pair p is frames 2p (previous) and 2p + 1 (current), each detected on its own.
+ * Records, matches and the pose tail are per pair exactly as after
+ * dvo_stream_process (the pair's outputs are identical: detection is a function
+ * of the frame).  2 n_pairs <= max_frames.  Used for the reference-equivalent
+ * timing leg of bench.py. */
+int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
+                             dvo_pair_record* d_records);
 /* dvo_stream_process on undistorted frames: the n raw frames are remapped by u
  * into the stream's own frame slab first (same HIP stream), as the reference
  * undistorts every frame before detection (v3:120, v3:135). */

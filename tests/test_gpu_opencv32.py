@@ -46,7 +46,8 @@ def test_pyramid_opencv32(gpu_ctx, oracle_mod, W, H):
         frames = rng.integers(0, 256, (2, H, W)).astype(np.uint8)
         K = np.array([[W, 0, W / 2], [0, W, H / 2], [0, 0, 1.0]])
     fs = FrameStream(W, H, K, nfeatures=500, max_frames=2, ctx=gpu_ctx, opencv="3.2")
-    fs.process(torch.from_numpy(np.ascontiguousarray(frames)).cuda())
+    dev_frames = torch.from_numpy(np.ascontiguousarray(frames)).cuda()  # get_pyramid(blurred) re-reads level 0
+    fs.process(dev_frames)
     fs.sync()
     want = oracle_mod.pyramid(frames[1], semantics=oracle_mod.OCV32)
     want_b = oracle_mod.pyramid(frames[1], blurred=True, semantics=oracle_mod.OCV32)
@@ -55,6 +56,7 @@ def test_pyramid_opencv32(gpu_ctx, oracle_mod, W, H):
             np.testing.assert_array_equal(fs.pyramid(1, l), want[l], err_msg=f"level {l}")
         np.testing.assert_array_equal(fs.pyramid(1, l, blurred=True), want_b[l], err_msg=f"blurred level {l}")
     fs.close()
+    del dev_frames
 
 
 @pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])

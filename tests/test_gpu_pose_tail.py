@@ -115,3 +115,34 @@ def test_pose_tail_from_stag_messages(gpu_ctx, oracle_mod):
                                        MARKER_LEN, P, T)
         np.testing.assert_allclose(T_abs[p], T, rtol=1e-9, atol=1e-12)
     fs.close()
+
+
+def test_pose_tail_after_caller_dropped_records(gpu_ctx):
+    """process() allocates the records; the caller drops them and allocates on
+    torch's stream before pose_tail.  The stream keeps the last records alive
+    (the tail reads them), so T_rel/T_abs equal a run that held them."""
+    import gc
+    import torch
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    frames, K = synth_frames(640, 480, range(4))
+    dev = torch.from_numpy(frames).cuda()
+    dc = torch.from_numpy(np.stack([marker_corners(i, K) for i in range(4)])).cuda()
+    fs = FrameStream(640, 480, K, nfeatures=500, max_frames=4, ctx=gpu_ctx)
+    fs.reset_pose()
+    kept = fs.process(dev)
+    want = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
+    fs.sync()
+    want = [t.clone() for t in want]
+    del kept
+    fs.reset_pose()
+    fs.process(dev)  # result dropped at once
+    gc.collect()
+    junk = [torch.full((4096,), 255, dtype=torch.uint8, device="cuda") for _ in range(16)]  # reuse freed blocks
+    got = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
+    junk += [torch.full((4096,), 255, dtype=torch.uint8, device="cuda") for _ in range(16)]
+    fs.sync()
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g.cpu().numpy(), w.cpu().numpy())
+    fs.close()
