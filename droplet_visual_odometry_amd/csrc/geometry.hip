@@ -1002,6 +1002,15 @@ __device__ __forceinline__ void dk_priority() {
 #define DVO_SCORE_F32 1  // single-precision decision with the f64 test for the undecided (SampsonF32)
 #endif
 constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
+// Deferred f64 Sampson tests per score block: the (model, point) pairs the
+// single-precision bounds leave undecided are listed in LDS while the waves
+// stream the chunks, and the whole block runs their f64 tests once, after the
+// last chunk (one latency round trip per block instead of one per wave-chunk
+// that met an undecided point).  A full list falls back to the inline test.
+#ifndef DVO_SCORE_DEFER
+#define DVO_SCORE_DEFER 1
+#endif
+constexpr int kScoreUnd = 1024;
 constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
@@ -1261,6 +1270,35 @@ constexpr int kDkNT = 256;
 constexpr int kDkBudgets[kDkMaxPasses - 1] = {DVO_DK_B0, DVO_DK_B1, DVO_DK_B2};
 constexpr int kDkPasses = DVO_DK_B0 == 0 ? 1 : DVO_DK_B1 == 0 ? 2 : DVO_DK_B2 == 0 ? 3 : 4;
 constexpr int kRecSnap = 108;                     // parked: Brent snapshot (20 doubles)
+#ifdef DVO_DK_STATS
+// Measurement build only: per pass, the sweeps run by each lane (useful work) and the
+// sweeps of each wave (its slowest lane: issued work), printed by dk_stats_kernel.
+constexpr int kDkStatWaves = 1 << 16;
+__device__ unsigned int g_dk_wave_max[kDkMaxPasses][kDkStatWaves];
+__device__ unsigned long long g_dk_lane_sum[kDkMaxPasses];
+__device__ __forceinline__ void dk_stat(int pass, int sweeps) {
+    atomicAdd(&g_dk_lane_sum[pass], (unsigned long long)sweeps);
+    const int w = (int)(blockIdx.x * (kDkNT / 64) + (threadIdx.x >> 6));
+    if (w < kDkStatWaves) atomicMax(&g_dk_wave_max[pass][w], (unsigned)sweeps);
+}
+__global__ void dk_stats_kernel(int round, int nwaves) {
+    for (int pass = 0; pass < kDkMaxPasses; ++pass) {
+        unsigned long long ws = 0, nw = 0;
+        for (int w = 0; w < min(nwaves, kDkStatWaves); ++w) {
+            ws += g_dk_wave_max[pass][w];
+            nw += g_dk_wave_max[pass][w] > 0;
+            g_dk_wave_max[pass][w] = 0;
+        }
+        if (ws)
+            printf("DKSTAT round %d pass %d lane_sweeps %llu wave_sweeps_x64 %llu waves %llu lane_eff %.4f\n", round, pass,
+                   g_dk_lane_sum[pass], ws * 64, nw, (double)g_dk_lane_sum[pass] / (double)(ws * 64));
+        g_dk_lane_sum[pass] = 0;
+    }
+}
+#define DK_STAT(pass, n) dk_stat(pass, n)
+#else
+#define DK_STAT(pass, n) ((void)0)
+#endif
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
     dk_priority();
@@ -1312,16 +1350,19 @@ void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
             R[kRecNr * 64] = (double)(br.it | br.saved_it << 9 | (31 - __clz(br.power)) << 18 | br.target << 22);
             const int slot = atomicAdd(&g.dk_ctl[2 + pass], 1);
             g.dk_list[(int64_t)pass * g.dk_list_cap + slot] = item;
+            DK_STAT(pass, sweep);
             return;
         }
         bool moved, same = false;
         dk_sweep<false>(c, roots, moved, same);
         if (same) {  // coincident roots: stage C redoes this polynomial exactly
             R[kRecGeneric * 64] = 2.0;
+            DK_STAT(pass, sweep + 1);
             return;
         }
         if (br.step(roots, moved)) {
             dk_store(R, roots);
+            DK_STAT(pass, sweep + 1);
             return;
         }
     }
@@ -1551,6 +1592,10 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     __shared__ float4 s_ptf[kScoreChunk];
     __shared__ float s_sf[HYPS * 10][12];  // SampsonF32 of each model: e[9], mk, ok
     __shared__ int s_moff[HYPS * 10];      // the model's offset in g.models (the f64 test)
+#if DVO_SCORE_DEFER
+    __shared__ uint32_t s_und[kScoreUnd];  // deferred f64 tests: model << 16 | point, ~0u = void slot
+    __shared__ int s_nund;
+#endif
 #endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
     static_assert(HYPS < 64, "one wave prefixes the model counts; lane hn (< 64) writes the total");
@@ -1564,6 +1609,9 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         }
         if (tid <= hn) s_pref[tid] = x - c;
     }
+#if DVO_SCORE_F32 && DVO_SCORE_DEFER
+    if (tid == 0) s_nund = 0;
+#endif
     __syncthreads();
     const int T = s_pref[hn];
 #if !DVO_SCORE_F32
@@ -1629,6 +1677,28 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
                 cnt += __popcll(__ballot(d == 1));
                 umask |= (uint32_t)(d < 0) << k;
             }
+#if DVO_SCORE_DEFER
+            if (m <= 0x10000 && __ballot(umask != 0)) {  // list the chunk's undecided points for the block's f64 pass
+#pragma unroll
+                for (int k = 0; k < kScoreChunk / 64; ++k) {
+                    const bool u = (umask >> k) & 1u;
+                    const unsigned long long bits = __ballot(u);
+                    if (bits == 0) continue;  // wave-uniform
+                    const int n = __popcll(bits);
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&s_nund, n);
+                    base = __shfl(base, 0);
+                    const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                               (uint32_t)(bits >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
+                    if (base + n <= kScoreUnd) {
+                        if (u) s_und[pos] = (uint32_t)e << 16 | (uint32_t)(c0 + lane + 64 * k);
+                        umask &= ~(1u << k);
+                    } else if (u && pos < kScoreUnd) {
+                        s_und[pos] = ~0u;  // the reservation straddles the end: its slots stay void
+                    }
+                }
+            }
+#endif
 #ifndef DVO_EXP_SCORE_NO_F64  // timing experiment only: undecided points counted as outliers
             if (__ballot(umask != 0)) {
                 double Ed[9];
@@ -1658,6 +1728,22 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         }
     }
     __syncthreads();
+#if DVO_SCORE_F32 && DVO_SCORE_DEFER
+    {  // the block's deferred f64 tests, all at once
+        const int nu = min(s_nund, kScoreUnd);
+        for (int u = tid; u < nu; u += kScoreNT) {
+            const uint32_t w = s_und[u];
+            if (w == ~0u) continue;
+            const int e = (int)(w >> 16), j = (int)(w & 0xFFFFu);
+            double Ed[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Ed[k] = g.models[hbase * 90 + s_moff[e] + k];
+            const double* pt = npts + (int64_t)j * 4;
+            if (sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok)) atomicAdd(&s_cnt[e], 1);
+        }
+        __syncthreads();
+    }
+#endif
     for (int e = tid; e < T; e += kScoreNT) {
         int h = 0;
         while (h + 1 < hn && s_pref[h + 1] <= e) ++h;
@@ -1859,6 +1945,9 @@ hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) 
             for (int pass = 0; pass < kDkPasses; ++pass)
                 hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
                                    pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
+#ifdef DVO_DK_STATS
+            hipLaunchKernelGGL(dk_stats_kernel, dim3(1), dim3(1), 0, s, round, (int)dgrid.x * (kDkNT / 64));
+#endif
         }
         if (one)
             hipLaunchKernelGGL(ransac_stage_c_row_kernel, dim3((span + 3) / 4, pairs), dim3(64), 0, s, g);
