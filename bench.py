@@ -91,6 +91,9 @@ def parse():
                     help="skip the reference-equivalent leg (both frames of every pair detected, GPU and CPU)")
     ap.add_argument("--no-host-fed", action="store_true",
                     help="skip the host-fed leg (pinned host frames, async H2D on a copy stream)")
+    ap.add_argument("--tail-world", type=int, default=8,
+                    help="rehearse rank 0's reassembly load of a world-N window at N=1: the pose tail and absolute "
+                         "chain over N x B gathered records on torch's stream beside the library streams (0 = skip)")
     ap.add_argument("--pose-check-32", type=int, default=24,
                     help="pairs of the OpenCV 3.2-semantics pose check against the oracle (0 = skip)")
     return ap.parse_args()
@@ -228,6 +231,11 @@ def main():
         for f in fss:
             f.set_profiling(False)
         legs["host_fed"] = host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, value)
+    if args.tail_world > 1:
+        for f in fss:
+            f.set_profiling(False)
+        legs[f"rank0_tail_world{args.tail_world}"] = rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows,
+                                                                    scene.K, ctx)
 
     cpu = None
     pose_check = None
@@ -433,6 +441,77 @@ def host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, stre
             "vs_device_resident": round(value / stream_value, 4),
             "schedule": "pinned host frames, async H2D on a copy stream into a ring of S+1 device slots "
                         "overlapped with compute; B+1 frames copied per B-pair step"}
+
+
+def rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows, K, ctx):
+    """Rank 0's added load in a world-N run (bench.main_sharded, dist.ShardedStreamRunner), rehearsed on one
+    GPU: per step the library streams process B new pairs as every rank does, and torch's stream -- after
+    waiting for that step's records, as before the all-gather -- runs the pose tail and the serial absolute
+    chain over a whole world-N window, N x B records (stream.PoseTail / dvo_pose_tail_records), as rank 0
+    does after the collective.  The gathered window is this rank's B records and corners tiled N times (the
+    tail's cost does not depend on their values).  Reported: ms per step with and without the rank-0 tail
+    and the difference, against north_star's near-linear scaling (trajectory_evaluation_dual_process.py:
+    172-252 is the single stream being reassembled)."""
+    import torch
+    from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
+    from droplet_visual_odometry_amd.stream import PoseTail
+    from droplet_visual_odometry_amd.synth import MARKER_LEN
+    B, S, N = args.batch, len(fss), args.tail_world
+    dev = pool.device
+    rb = PAIR_RECORD_DTYPE.itemsize
+    wrecs = [torch.cat([recs_t[k][:B * rb]] * N).contiguous() for k in range(S)]
+    cp = corners[:B].repeat(N, 1, 1).contiguous()
+    cc = corners[1:B + 1].repeat(N, 1, 1).contiguous()
+    tail = PoseTail(K, MARKER_LEN, ctx=ctx)
+    T_rel = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_abs = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    cur = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()
+
+    def run(with_tail):
+        def step(i):
+            s0, k = (i % n_windows) * B, i % S
+            fs = fss[k]
+            fs.wait_event(getattr(fs, "_tail_done", None))  # the slot's records were read by its last tail
+            fs.process(pool[s0:s0 + B + 1], recs_t[k], wait_torch=False)
+            if with_tail:
+                cur.wait_event(fs.record_event())  # the records are final (before the collective)
+                wrecs[k][:B * rb].copy_(recs_t[k][:B * rb])
+                tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                fs._tail_done = ev
+
+        for i in range(args.warmup):
+            step(i)
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i)
+        for f in fss:
+            f.sync()
+        torch.cuda.synchronize()
+        for f in fss:
+            f._tail_done = None
+        return 1e3 * (time.perf_counter() - t0) / args.steps
+
+    base = run(False)
+    with_tail = run(True)
+    # the tail's own duration on an otherwise idle GPU (one launch of pose_tail + pose_chain over N x B records)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cur)
+    tail.run(wrecs[0], cp, cc, T_rel[0], T_abs[0])
+    e1.record(cur)
+    torch.cuda.synchronize()
+    alone = e0.elapsed_time(e1)
+    return {"world": N, "pairs_per_window": N * B, "ms_per_step_without_tail": round(base, 3),
+            "ms_per_step_with_tail": round(with_tail, 3), "added_ms_per_step": round(with_tail - base, 3),
+            "added_frac": round((with_tail - base) / base, 4), "tail_alone_ms": round(alone, 3),
+            "note": "rank 0's pose tail + serial absolute chain over a world-N window (N x B gathered records) on "
+                    "torch's stream beside the library streams; steps of B new pairs per rank (weak scaling)"}
 
 
 def pose_check_opencv32(pool, K, nfeatures, max_iters, n_pairs, ctx):

@@ -111,6 +111,7 @@ _SIGNATURES = {
     "dvo_stream_destroy": ([_vp], None),
     "dvo_stream_process": ([_vp, _vp, _c, _i64, _c, _vp], _c),
     "dvo_stream_process_pairs": ([_vp, _vp, _c, _i64, _c, _vp], _c),
+    "dvo_stream_pair": ([_vp, _vp, _vp, _c, _c, _vp], _c),
     "dvo_stream_sync": ([_vp], _c),
     "dvo_stream_hip_stream": ([_vp], _vp),
     "dvo_stream_set_profiling": ([_vp, _c], _c),

@@ -71,6 +71,13 @@ struct dvo_stream {
     int64_t last_fstride = 0;
     int last_pitch = 0;
     hipStream_t hs = nullptr;
+    // dvo_stream_pair: the last pair's current-frame features (the next pair's previous frame) and
+    // the device record of one pair, allocated by the first call
+    dvo_keypoint* fc_kps = nullptr;
+    uint8_t* fc_desc = nullptr;
+    int32_t* fc_n = nullptr;  // nkp, status
+    dvo_pair_record* pair_rec = nullptr;
+    bool fc_valid = false;
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
     std::vector<std::vector<hipEvent_t>> ev_pending;
@@ -750,6 +757,80 @@ int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs
     if (n_pairs < 1 || 2 * (int64_t)n_pairs > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_pairs out of range");
     if (!d_records) return fail(ctx, DVO_EINVAL, "null records");
     return process_frames(s, d_frames, 2 * n_pairs, frame_stride, stride, d_records, 2);
+}
+
+// One pair of host frames through the whole per-pair path in one synchronous call
+// (dvo.h dvo_stream_pair).  Slot 0 of the stream's frame slab / feature buffers is the
+// previous frame, slot 1 the current one.  With reuse_prev the current frame is detected
+// alone (as frame 0, the ORB kernels' per-call launch shapes), its features are moved
+// to slot 1 and the cached ones of the last call's current frame to slot 0; then the
+// matcher (train stages split over workgroups: one pair alone fills the chip), the
+// per-call RANSAC schedule (one round, 16-lane Durand-Kerner), recoverPose and the
+// record, and one device-to-host copy of the record.
+int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_img, int stride, int reuse_prev,
+                    dvo_pair_record* rec_out) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    const int w = s->cfg.width, h = s->cfg.height;
+    if (s->cfg.max_frames < 2) return fail(ctx, DVO_EINVAL, "dvo_stream_pair needs max_frames >= 2");
+    if (!cur_img || !rec_out || stride < w || (!reuse_prev && !prev_img)) return fail(ctx, DVO_EINVAL, "bad image buffer");
+    if (reuse_prev && !s->fc_valid) return fail(ctx, DVO_EINVAL, "reuse_prev needs a preceding dvo_stream_pair");
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t kc = (size_t)s->plan.kp_cap;
+    if (!s->fc_kps) {
+        int rc;
+        if ((rc = dalloc(s, &s->fc_kps, kc)) || (rc = dalloc(s, &s->fc_desc, kc * 32)) ||
+            (rc = dalloc(s, &s->fc_n, 2)) || (rc = dalloc(s, &s->pair_rec, 1)))
+            return rc;
+    }
+    Staging st;
+    int rc = staging(ctx, Staging::round(sizeof(dvo_pair_record)), s->hs, &st);
+    if (rc) return rc;
+    const int pw = frame_pitch(s);
+    const int64_t fst = (int64_t)pw * h;
+    const Buffers& b = s->buf;
+    // slot a's features -> slot b's (keypoints, descriptors, count, status)
+    auto move_feats = [&](const dvo_keypoint* k0, const uint8_t* d0, const int32_t* n0, const int32_t* st0,
+                          dvo_keypoint* k1, uint8_t* d1, int32_t* n1, int32_t* st1) -> hipError_t {
+        hipError_t e;
+        if ((e = hipMemcpyAsync(k1, k0, kc * sizeof(dvo_keypoint), hipMemcpyDeviceToDevice, s->hs)) != hipSuccess ||
+            (e = hipMemcpyAsync(d1, d0, kc * 32, hipMemcpyDeviceToDevice, s->hs)) != hipSuccess ||
+            (e = hipMemcpyAsync(n1, n0, sizeof(int32_t), hipMemcpyDeviceToDevice, s->hs)) != hipSuccess)
+            return e;
+        return hipMemcpyAsync(st1, st0, sizeof(int32_t), hipMemcpyDeviceToDevice, s->hs);
+    };
+    if (reuse_prev) {
+        HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, cur_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+        if ((rc = run_stream(s, s->d_frames, 1, fst, pw, nullptr, true))) return rc;
+        HIP_TRY(move_feats(b.kps, b.desc, b.nkp, b.status, b.kps + kc, b.desc + kc * 32, b.nkp + 1, b.status + 1));
+        HIP_TRY(move_feats(s->fc_kps, s->fc_desc, s->fc_n, s->fc_n + 1, b.kps, b.desc, b.nkp, b.status));
+    } else {
+        HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, prev_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+        HIP_TRY(hipMemcpy2DAsync(s->d_frames + fst, pw, cur_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+        if ((rc = run_stream(s, s->d_frames, 2, fst, pw, nullptr, true))) return rc;
+    }
+    // the current frame's features are the next pair's previous frame
+    HIP_TRY(move_feats(b.kps + kc, b.desc + kc * 32, b.nkp + 1, b.status + 1, s->fc_kps, s->fc_desc, s->fc_n,
+                       s->fc_n + 1));
+    StreamParams P = params_of(s, s->d_frames, 2, fst, pw);
+    const int nqb = ((int)kc + 255) / 256, nst = ((int)kc + 63) / 64;
+    int tsplit = 1;
+    while (tsplit < 16 && nqb * tsplit * 2 <= 256 && nst >= tsplit * 8) tsplit *= 2;
+    HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, nullptr, tsplit));
+    HIP_TRY(launch_geometry(P, stream_geom(s), s->pair_rec, s->hs, nullptr, true));
+    uint8_t* hr = nullptr;
+    HIP_TRY(st.get(s->pair_rec, sizeof(dvo_pair_record), &hr));
+    HIP_TRY(hipStreamSynchronize(s->hs));
+    std::memcpy(rec_out, hr, sizeof(dvo_pair_record));
+    s->fc_valid = true;
+    s->last_nframes = 2;
+    s->last_pairs = 1;
+    s->last_has_pairs = true;
+    s->last_rec = s->pair_rec;
+    s->last_frames = s->d_frames;
+    s->last_fstride = fst;
+    s->last_pitch = pw;
+    return DVO_OK;
 }
 
 int dvo_stream_sync(dvo_stream* s) {

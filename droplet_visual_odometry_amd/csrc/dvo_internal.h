@@ -292,9 +292,12 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nul
 // reads a blurred pyramid (describe_blurs() false); otherwise for dvo_stream_get_pyramid(blurred).
 hipError_t launch_blur(const StreamParams& P, hipStream_t s);
 bool describe_blurs();
-hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev = nullptr);
+// tsplit > 1 splits every pair's train stages over tsplit workgroups (one pair alone fills the chip)
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev = nullptr, int tsplit = 1);
+// one_round: a single RANSAC round over every hypothesis up to maxIters on the 16-lane Durand-Kerner
+// (kStageOneRound, the per-call schedule: E, R, t are the same, n_hypotheses differs)
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
-                           hipEvent_t* ev = nullptr);
+                           hipEvent_t* ev = nullptr, bool one_round = false);
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
 // Undistortion (undistort.hip): camera K, distortion k1 k2 p1 p2 k3 k4 k5 k6 s1..s4.
 struct UndistortGeom {

@@ -2368,11 +2368,11 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
 }
 
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
-                           hipEvent_t* ev) {
+                           hipEvent_t* ev, bool one_round) {
     const int pairs = stream_pairs(P);
     if (pairs <= 0) return hipSuccess;
     mark(ev, 6, 0, s);
-    hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac, s);
+    hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac | (one_round ? kStageOneRound : 0), s);
     mark(ev, 6, 1, s);
     if (e != hipSuccess) return e;
     mark(ev, 7, 0, s);

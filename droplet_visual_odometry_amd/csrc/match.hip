@@ -320,7 +320,7 @@ __device__ int crosscheck_sort(const int32_t* fwd, const int32_t* bwd, int nq, i
     } else {
         for (int q = threadIdx.x; q < nq; q += kXNT) {
             int f = fwd[q];
-            if (f < 0) continue;
+            if (f < 0 || (f >> 16) > 256) continue;  // -1 or the untouched 0x7F7F7F7F fill (split trains, nt = 0)
             int t = f & 0xFFFF;
             if (mode == 1 && (bwd[t] & 0xFFFF) != q) continue;
             int slot = atomicAdd(&s_m, 1);
@@ -445,18 +445,21 @@ __global__ __launch_bounds__(kXNT) void crosscheck_pair_kernel(const int32_t* fw
 
 }  // namespace
 
-hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev) {
+hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev, int tsplit) {
     const int pairs = stream_pairs(P);
     if (pairs < 1) return hipSuccess;
     mark(ev, 5, 0, s);
     const int cap = P.plan.kp_cap;
-    // backward keys start at 0x7F7F7F7F ("none") and are lowered by atomicMin
-    hipError_t e = hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F, sizeof(int32_t) * (size_t)P.nframes * cap, s);
+    // backward keys (and, split, the forward keys) start at 0x7F7F7F7F ("none") and are lowered by atomicMin
+    hipError_t e = tsplit > 1
+                       ? hipMemsetAsync(P.buf.nn, 0x7F, sizeof(int32_t) * 2 * (size_t)P.nframes * cap, s)
+                       : hipMemsetAsync(P.buf.nn + (int64_t)P.nframes * cap, 0x7F,
+                                        sizeof(int32_t) * (size_t)P.nframes * cap, s);
     if (e != hipSuccess) return e;
     const int nqb = (cap + kMQB - 1) / kMQB;
-    const int nwg = ((pairs * nqb + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
+    const int nwg = ((pairs * nqb * tsplit + 7) / 8) * 8;  // XCD grouping needs a multiple of 8 blocks
     const NnOperands O{P.buf.desc, P.buf.desc + (int64_t)cap * 32, (int64_t)cap * 32, -1, -1};
-    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, O, pairs, nqb, 1);
+    hipLaunchKernelGGL(nn_mfma_kernel, dim3(nwg), dim3(256), 0, s, P, O, pairs, nqb, tsplit);
     hipLaunchKernelGGL(crosscheck_stream_kernel, dim3(pairs), dim3(kXNT), 0, s, P, cross_check);
     mark(ev, 5, 1, s);
     return hipGetLastError();

@@ -19,6 +19,15 @@ Behaviour notes versus the reference:
       frame when the same bytes come back.
   D6  drawKeypoints is returned lazily: the drawn image is made the first
       time a caller reads it (the reference computes it and discards it).
+  D7  fused pair path: with the stock ORB / BFMatcher(NORM_HAMMING, crossCheck)
+      operators (mode "orb", no method overridden), visual_odometry_calculations
+      runs detect -> match -> findEssentialMat -> recoverPose in ONE library
+      call (FrameStream.pair / dvo_stream_pair; the previous frame's features
+      stay on the device when its bytes come back as the next previous frame),
+      then the same host tail (triangulation, scale, Euler rebuild) as the
+      operator-by-operator path, so the 4x4s are identical.  Any pair the
+      library reports as failing (status, or not exactly one E) is redone
+      operator by operator, which raises where the reference raises.
 
 Matches and keypoints are array-backed sequences (cv.DMatches, cv.KeyPoints):
 the ORB branch sorts by distance with a stable argsort (Python's sorted() is
@@ -144,6 +153,8 @@ class VisualOdometry:
         self.projection_matrix_list = []
         self.plot_4D_counter = 1
         self._features = _FeatureCache()
+        self._pair_engine = None  # (config key, FrameStream) of the fused pair path (D7)
+        self._pair_last = None    # content key of the last fused pair's current frame
         self.robot_curr_position = self.make_transform_mat(translation=self.starting_translation,
                                                            euler=self.starting_euler)
 
@@ -274,6 +285,12 @@ class VisualOdometry:
                                                                       points1=array_previous_key_points,
                                                                       points2=array_current_key_points,
                                                                       cameraMatrix=K)
+        return self._relative_transform(relative_rotation, translation, previous_marker_corners,
+                                        current_marker_corners)
+
+    def _relative_transform(self, relative_rotation, translation, previous_marker_corners, current_marker_corners):
+        """v3:305-345: P_cur = K [R | t], marker scale, 4x4 previous->current."""
+        K = self.intrinsic_coefficient_matrix
         current_projection_matrix = K.dot(np.hstack((relative_rotation, translation.reshape(-1, 1))))
         distance = self.get_scaling_factor_from_triangulation(current_projection_matrix=current_projection_matrix,
                                                               previous_marker_corners=previous_marker_corners,
@@ -307,9 +324,54 @@ class VisualOdometry:
             self._features.put(key, hit)
         return hit
 
+    def _fused_pair(self, previous_image, current_image):
+        """(E, R, t) of the pair from one library call (D7), or None when the
+        stock operators are not in use or the library reports a failing pair."""
+        cls = type(self)
+        if (self.mode != "orb" or type(self.feature_detector) is not cv.ORB or type(self.bf) is not cv.BFMatcher
+                or self.bf.normType != cv.NORM_HAMMING or not self.bf.crossCheck
+                or any(getattr(cls, m) is not getattr(VisualOdometry, m) for m in (
+                    "compute_current_image_elements", "get_matches_between_two_frames", "previous_current_matching",
+                    "get_transformation_between_two_frames"))):
+            return None
+        prev = np.asarray(previous_image)
+        cur = np.asarray(current_image)
+        if prev.dtype != np.uint8 or cur.dtype != np.uint8 or prev.ndim != 2 or prev.shape != cur.shape:
+            return None
+        h, w = cur.shape
+        if not (8 <= w < 4096 and 8 <= h < 4096):
+            return None
+        K = np.ascontiguousarray(self.intrinsic_coefficient_matrix, np.float64)
+        if K.shape != (3, 3):
+            return None
+        det = self.feature_detector
+        cc = 2 if self.bf.legacy_crosscheck else 1
+        cfg = (w, h, det.nfeatures, det.fastThreshold, det.opencv, K.tobytes(), cc)
+        if self._pair_engine is None or self._pair_engine[0] != cfg:
+            from droplet_visual_odometry_amd import ops
+            self._pair_engine = None
+            self._pair_last = None
+            self._pair_engine = (cfg, ops.PairStream(w, h, K, nfeatures=det.nfeatures, fast_threshold=det.fastThreshold,
+                                                     cross_check=cc, opencv=det.opencv))
+        fs = self._pair_engine[1]
+        kprev, kcur = _FeatureCache.key(prev), _FeatureCache.key(cur)
+        reuse = self._pair_last is not None and self._pair_last == kprev
+        self._pair_last = None
+        rec = fs.pair(None if reuse else prev, cur, reuse_prev=reuse)
+        self._pair_last = kcur
+        if rec["status"] != 0 or rec["n_models"] != 1:
+            return None
+        return rec["E"].reshape(3, 3).copy(), rec["R"].reshape(3, 3).copy(), rec["t"].reshape(3, 1).copy()
+
     def visual_odometry_calculations(self, previous_image, current_image, robot_previous_position_transformation,
                                      previous_marker_corners, current_marker_corners):
         """(T_robot_current, T_previous_to_current) for one frame pair (v3:384-408)."""
+        fused = self._fused_pair(previous_image, current_image)
+        if fused is not None:  # D7: detect -> match -> E -> R, t in one call, then the same host tail
+            self.essential_matrix, relative_rotation, translation = fused
+            rel = self._relative_transform(relative_rotation, translation, previous_marker_corners,
+                                           current_marker_corners)
+            return robot_previous_position_transformation.dot(rel), rel
         prev_kp, prev_desc, _ = self.compute_current_image_elements(previous_image)
         cur_kp, cur_desc, _ = self.compute_current_image_elements(current_image)
         _matches, top_prev, top_cur = self.get_matches_between_two_frames(

@@ -20,8 +20,8 @@ import ctypes
 
 import numpy as np
 
-from ._native import (DMATCH_DTYPE, DVO_ECAP, DVO_OK, KEYPOINT_DTYPE, Context, DVOError, load_library, orb_params,
-                      ptr)
+from ._native import (DMATCH_DTYPE, DVO_ECAP, DVO_OK, KEYPOINT_DTYPE, PAIR_RECORD_DTYPE, Context, DVOError, StreamConfig,
+                      load_library, orb_params, ptr)
 
 
 def _ctx(ctx):
@@ -333,6 +333,58 @@ class Undistorter:
         if getattr(self, "h_", None):
             self.ctx.lib.dvo_undistort_destroy(self.h_)
             self.h_ = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PairStream:
+    """One pair of host frames per call through the whole per-pair path
+    (dvo_stream_pair): detectAndCompute of both frames, BFMatcher.match with
+    crossCheck, findEssentialMat(RANSAC, prob, threshold, maxIters) and
+    recoverPose (visual_odometry_v3.py:384-408 up to v3:303) in one
+    synchronous library call, the 256-B pair record back.  With
+    reuse_prev=True the previous frame is the last call's current frame and
+    only the current one is detected.  The drop-in's fused path (D7) uses it;
+    no torch involved."""
+
+    def __init__(self, width, height, K, nfeatures=500, fast_threshold=20, cross_check=1, opencv="4.x", prob=0.999,
+                 threshold=1.0, max_iters=1000, dist_thresh=50.0, ctx=None):
+        self.ctx = _ctx(ctx)
+        cfg = StreamConfig()
+        cfg.width, cfg.height, cfg.max_frames = int(width), int(height), 2
+        cfg.orb = orb_params(nfeatures=nfeatures, fast_threshold=fast_threshold, opencv=opencv)
+        K = np.asarray(K, np.float64).reshape(9)
+        for i in range(9):
+            cfg.K[i] = float(K[i])
+        cfg.prob, cfg.threshold, cfg.max_iters = float(prob), float(threshold), int(max_iters)
+        cfg.cross_check, cfg.dist_thresh = int(cross_check), float(dist_thresh)
+        h = ctypes.c_void_p()
+        self.ctx.check(self.ctx.lib.dvo_stream_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        self.width, self.height = int(width), int(height)
+
+    def pair(self, prev_img, cur_img, reuse_prev=False) -> np.ndarray:
+        cur = np.ascontiguousarray(cur_img, np.uint8)
+        if cur.shape != (self.height, self.width):
+            raise ValueError(f"frame shape {cur.shape} != {(self.height, self.width)}")
+        prev = None
+        if not reuse_prev:
+            prev = np.ascontiguousarray(prev_img, np.uint8)
+            if prev.shape != cur.shape:
+                raise ValueError("previous and current frames differ in shape")
+        rec = np.zeros(1, PAIR_RECORD_DTYPE)
+        self.ctx.check(self.ctx.lib.dvo_stream_pair(self.h, ptr(prev), ptr(cur), self.width, int(bool(reuse_prev)),
+                                                    ptr(rec)))
+        return rec[0]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.dvo_stream_destroy(self.h)
+            self.h = None
 
     def __del__(self):
         try:

@@ -230,6 +230,20 @@ int dvo_stream_sync(dvo_stream* s);
  * timing leg of bench.py. */
 int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
                              dvo_pair_record* d_records);
+/* One pair of HOST frames through the whole per-pair path in one synchronous
+ * call: the device half of visual_odometry_calculations (v3:384-408) up to
+ * recoverPose (v3:303) -- detectAndCompute of both frames (v3:387-392),
+ * BFMatcher.match + crossCheck (v3:219), findEssentialMat(RANSAC, 0.999, 1.0)
+ * (v3:297) and recoverPose (v3:303) -- returning the pair's record (R, t, E,
+ * counts, status) in rec_out.  It replaces the drop-in's six separate operator
+ * calls per pair (their host round trips and Python glue) with one; E, R and t
+ * equal the operator-by-operator path's (the per-call RANSAC schedule: one
+ * round, n_hypotheses as dvo_find_essential_mat).  reuse_prev = 1: the
+ * previous frame is the last call's current frame, whose features the stream
+ * kept on the device (prev_img may be NULL), so only cur_img is detected.
+ * Images: w x h mono8, rows `stride` bytes apart.  Needs max_frames >= 2. */
+int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_img, int stride, int reuse_prev,
+                    dvo_pair_record* rec_out);
 /* dvo_stream_process on undistorted frames: the n raw frames are remapped by u
  * into the stream's own frame slab first (same HIP stream), as the reference
  * undistorts every frame before detection (v3:120, v3:135). */

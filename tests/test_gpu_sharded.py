@@ -134,15 +134,17 @@ def test_sharded_stream_equals_single_rank(gpu_ctx, W, H, NF, n_pairs, windows, 
     _check(gpu_ctx, out, 2, W, H, NF, F, blank)
 
 
-def test_sharded_rccl_path_two_slots_in_flight(gpu_ctx):
+@pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])
+def test_sharded_rccl_path_two_slots_in_flight(gpu_ctx, W, H, NF):
     """The RCCL branch of the sharded loop (device all-gather, no host syncs):
     world size 1 on the box's one GPU, two send-buffer slots in flight over six
     windows, so every slot is rewritten while the previous windows' collectives
     and pose tails are still queued.  Any missing stream order (records read
     before written, a send buffer rewritten before its collective read it, the
-    tail racing the gather) shows as a mismatch with the single-rank stream."""
+    tail racing the gather) shows as a mismatch with the single-rank stream.
+    Also at BASELINE configs[3]'s 1280x720 / 2000 features."""
     import torch.multiprocessing as mp
-    W, H, NF, n_pairs, windows, blank = 640, 480, 500, 8, 6, (12,)
+    n_pairs, windows, blank = 8, 6, (12,)
     F = n_pairs * windows + 1
     mgr = mp.Manager()
     out = mgr.dict()
