@@ -1011,6 +1011,14 @@ constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 #define DVO_SCORE_DEFER 1
 #endif
 constexpr int kScoreUnd = 1024;
+// Early exit of a model that cannot matter: the replay changes state only at a count above
+// max(maxgood, 4) of the rounds before (RANSACPointSetRegistrator::run's test, ptsetreg.cpp), so
+// once a model's count so far plus its deferred tests plus the points not yet scored is <= that
+// bound, its final count is too, and it stops being scored (the partial count it stores is <= the
+// bound as well: the replay cannot tell the difference).  Round 2 starts from round 1's maxgood.
+#ifndef DVO_SCORE_BAIL
+#define DVO_SCORE_BAIL 1
+#endif
 constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
@@ -1595,6 +1603,7 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
 #if DVO_SCORE_DEFER
     __shared__ uint32_t s_und[kScoreUnd];  // deferred f64 tests: model << 16 | point, ~0u = void slot
     __shared__ int s_nund;
+    __shared__ int s_pend[HYPS * 10];      // deferred tests per model (possible inliers not yet counted)
 #endif
 #endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
@@ -1623,6 +1632,10 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     }
 #endif
     for (int e = tid; e < T; e += kScoreNT) s_cnt[e] = 0;
+#if DVO_SCORE_F32 && DVO_SCORE_DEFER
+    for (int e = tid; e < T; e += kScoreNT) s_pend[e] = 0;
+#endif
+    const int bail = max(S.maxgood, 4);  // a final count <= bail never changes the replay
     const double thr = g.threshold / ((g.fx + g.fy) / 2);
     const float t = (float)(thr * thr);
     const bool fast_ok = t >= FLT_MIN;  // the division-free test needs t normal
@@ -1658,6 +1671,9 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         // one wave per model (2 or 4 models per wave pass over the chunk, reading each point
         // once, measured slower: 73.0 K vs 72.6 / 71.4 K frames/s, profiles/r02w_ab_score_dk.txt)
         for (int e = wid; e < T; e += kScoreNT / 64) {
+#if DVO_SCORE_BAIL && DVO_SCORE_F32 && DVO_SCORE_DEFER
+            if (s_cnt[e] + s_pend[e] + (m - c0) <= bail) continue;  // wave-uniform: this wave's own model
+#endif
             int cnt = 0;
 #if DVO_SCORE_F32
             // undecided points (a sliver) are marked per lane and take the f64 test after the
@@ -1692,6 +1708,7 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
                                                (uint32_t)(bits >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
                     if (base + n <= kScoreUnd) {
                         if (u) s_und[pos] = (uint32_t)e << 16 | (uint32_t)(c0 + lane + 64 * k);
+                        if (lane == 0) s_pend[e] += n;
                         umask &= ~(1u << k);
                     } else if (u && pos < kScoreUnd) {
                         s_und[pos] = ~0u;  // the reservation straddles the end: its slots stay void

@@ -143,6 +143,7 @@ __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l
 // coalesced word loads (lane k <- word k), then every lane reads its 3 words
 // per source row from LDS.  Same arithmetic as resize_level_kernel.
 constexpr int kRsLR = 8;  // output rows per wave (32 per workgroup)
+
 constexpr int kRsW = 96, kRsLRows = 44;  // 32 * 1.25 + 2 source rows, padded to a multiple of 4
 
 // 1-D grids of (frame, item) blocks, XCD-grouped: workgroups are dispatched
@@ -165,6 +166,63 @@ __device__ __forceinline__ int xcd_frame_item(int nitems, int nframes, int& item
     return (blockIdx.x & 7) + 8 * fq;
 }
 
+// Per-lane constants of one destination word (4 pixels) of the LDS-staged resize: the staged
+// source words it reads (wb0 .. wb0 + 2 of a window starting at source column sx0), the byte shift
+// of its first tap, and per output pixel j a v_perm selector giving the u16 pair (src[o_j],
+// src[o_j + 1]) and the pair of weights (256 - c1, c1) for v_dot2_u32_u16.  The 4 taps of a lane span
+// <= 6 bytes at ratio <= 1.25.  x0: the word's first destination column; dw: the destination width;
+// maxw: the staged row's word count (lanes past the level's right edge read any in-range words).
+struct RsLane {
+    int wb0, sh;
+    uint32_t sel[4], kw[4];
+};
+__device__ __forceinline__ RsLane rs_lane(const int32_t* cxt, int x0, int dw, int sx0, int maxw) {
+    const int4 cx = *reinterpret_cast<const int4*>(cxt + min(x0, ((dw + 3) & ~3) - 4));
+    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w};
+    int i0[4], c1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        i0[j] = coef_ofs(cxs[j]) - sx0;
+        c1[j] = coef_c1(cxs[j]);
+    }
+    RsLane L;
+    L.wb0 = min(i0[0] >> 2, maxw - 3);
+    const int base = 4 * L.wb0;
+    L.sh = min(i0[0] - base, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t r = (uint32_t)min(max(i0[j] - base - L.sh, 0), 6);
+        L.sel[j] = 0x0C000C00u | r | ((r + 1) << 16);
+        L.kw[j] = (uint32_t)(256 - c1[j]) | ((uint32_t)c1[j] << 16);
+    }
+    return L;
+}
+// One destination word from two staged source rows a (ofs) and b (ofs + 1) and the row weights
+// ky = (256 - cy1) | cy1 << 16: h = (256 - c1) s[o] + c1 s[o + 1] <= 65280 per row, then
+// h0 (256 - cy1) + h1 cy1 + 2^15 < 2^24, whose byte 2 is the pixel (INTER_LINEAR_EXACT).
+__device__ __forceinline__ uint32_t rs_word(const uint32_t* a, const uint32_t* b, const RsLane& L, uint32_t ky) {
+    const uint32_t a0 = a[L.wb0], a1 = a[L.wb0 + 1], a2 = a[L.wb0 + 2];
+    const uint32_t b0 = b[L.wb0], b1 = b[L.wb0 + 1], b2 = b[L.wb0 + 2];
+    const uint32_t alo = __builtin_amdgcn_alignbyte(a1, a0, L.sh), ahi = __builtin_amdgcn_alignbyte(a2, a1, L.sh);
+    const uint32_t blo = __builtin_amdgcn_alignbyte(b1, b0, L.sh), bhi = __builtin_amdgcn_alignbyte(b2, b1, L.sh);
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t h0 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(ahi, alo, L.sel[j])),
+                                                   as_u16x2(L.kw[j]), 0u, false);
+        const uint32_t h1 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(bhi, blo, L.sel[j])),
+                                                   as_u16x2(L.kw[j]), 0u, false);
+        v[j] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u)), as_u16x2(ky), 32768u,
+                                      false);
+    }
+    return __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[3], v[2], 0x0C0C0602u),
+                                 __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0602u), 0x05040100u);
+}
+__device__ __forceinline__ uint32_t rs_ky(int c) {
+    const uint32_t cy1 = coef_c1(c);
+    return (256u - cy1) | (cy1 << 16);
+}
+
 __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l, int gx) {
     __shared__ uint32_t tile[kRsLRows][kRsW];
     int item;
@@ -185,11 +243,8 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int32_t* cyt = P.buf.coef + D.ycoef_off;
     // source window of the tile (wave-uniform)
     const int sx0 = coef_ofs(cxt[xa]) & ~3;
-    const int nw = ((coef_ofs(cxt[min(xa + 255, D.w - 1)]) + 1 - sx0) >> 2) + 1;
     const int sy0 = coef_ofs(cyt[ty0]);
     const int nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsLR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
-    // this lane's taps (issued before the staging so their latency overlaps it)
-    const int4 cx = *reinterpret_cast<const int4*>(cxt + min(x0, ((D.w + 3) & ~3) - 4));
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
     {  // kRsLRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
         uint32_t v0[kRsLRows / 4], v1[kRsLRows / 4];
@@ -205,62 +260,23 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
             if (lane + 64 < kRsW) tile[wid + 4 * it][lane + 64] = v1[it];
         }
     }
+    // this lane's taps (their latency overlaps the staging)
+    const RsLane L = rs_lane(cxt, x0, D.w, sx0, kRsW);
     __syncthreads();
     const int dy0 = ty0 + wid * kRsLR;
     if (dy0 >= D.h) return;
     const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform (table padded to 8 rows)
     const int4 cz = *reinterpret_cast<const int4*>(cyt + dy0 + 4);
-    const int cxs[4] = {cx.x, cx.y, cx.z, cx.w};
     const int cys[kRsLR] = {cy.x, cy.y, cy.z, cy.w, cz.x, cz.y, cz.z, cz.w};
     static_assert(kRsLR == 8, "two int4 row-coefficient loads");
-    int i0[4], c1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        i0[j] = coef_ofs(cxs[j]) - sx0;
-        c1[j] = coef_c1(cxs[j]);
-    }
-    const int wb0 = min(i0[0] >> 2, kRsW - 3);  // lanes past the level's right edge: any in-range words
-    const int base = 4 * wb0;
     const bool full = x0 + 4 <= D.w;
-    // Per-lane constants for all rows: the 8-byte source window starting at the
-    // lane's first tap (v_alignbyte of the 3 staged words), and per output
-    // pixel j a v_perm selector giving the u16 pair (src[o_j], src[o_j + 1])
-    // and the pair of weights (256 - c1, c1) for v_dot2_u32_u16.  The 4 taps of
-    // a lane span <= 6 bytes at ratio <= 1.25.
-    const int sh = min(i0[0] - base, 3);
-    uint32_t sel[4], kw[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t r = (uint32_t)min(max(i0[j] - base - sh, 0), 6);
-        sel[j] = 0x0C000C00u | r | ((r + 1) << 16);
-        kw[j] = (uint32_t)(256 - c1[j]) | ((uint32_t)c1[j] << 16);
-    }
 #pragma unroll
     for (int rr = 0; rr < kRsLR; ++rr) {
         const int dy = dy0 + rr;
         if (dy >= D.h) break;
         const int lr = coef_ofs(cys[rr]) - sy0;
-        const uint32_t cy1 = coef_c1(cys[rr]);
-        const uint32_t ky = (256u - cy1) | (cy1 << 16);
         const int lr1 = min(lr + 1, kRsLRows - 1);  // weight-0 row past the window: any in-range row
-        const uint32_t a0 = tile[lr][wb0], a1 = tile[lr][wb0 + 1], a2 = tile[lr][wb0 + 2];
-        const uint32_t b0 = tile[lr1][wb0], b1 = tile[lr1][wb0 + 1], b2 = tile[lr1][wb0 + 2];
-        const uint32_t alo = __builtin_amdgcn_alignbyte(a1, a0, sh), ahi = __builtin_amdgcn_alignbyte(a2, a1, sh);
-        const uint32_t blo = __builtin_amdgcn_alignbyte(b1, b0, sh), bhi = __builtin_amdgcn_alignbyte(b2, b1, sh);
-        uint32_t v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            // h = (256 - c1) * s[o] + c1 * s[o + 1] <= 65280; then the rows: h0 (256 - cy1) + h1 cy1 + 2^15 < 2^24
-            const uint32_t h0 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(ahi, alo, sel[j])),
-                                                       as_u16x2(kw[j]), 0u, false);
-            const uint32_t h1 = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(bhi, blo, sel[j])),
-                                                       as_u16x2(kw[j]), 0u, false);
-            v[j] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(h1, h0, 0x05040100u)), as_u16x2(ky), 32768u,
-                                          false);
-        }
-        // byte 2 of each sum (< 2^24, so it is (sum >> 16) <= 255)
-        const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(v[3], v[2], 0x0C0C0602u),
-                                                    __builtin_amdgcn_perm(v[1], v[0], 0x0C0C0602u), 0x05040100u);
+        const uint32_t word = rs_word(tile[lr], tile[lr1], L, rs_ky(cys[rr]));
         uint8_t* drow = dst + (int64_t)dy * D.pitch;
         if (full) {
             *reinterpret_cast<uint32_t*>(drow + x0) = word;
@@ -1808,15 +1824,16 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const Plan& pl = P.plan;
     const int F = P.nframes;
     mark(ev, 0, 0, s);
+    // staged tiles fit when both ratios are <= 1.25: 256 * 1.25 + 12 bytes <= kRsW words,
+    // 32 * 1.25 + 2 rows <= kRsRows
+    auto lds_ok = [&](int l) { return 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h; };
     for (int l = 1; l < pl.nlevels; ++l) {
         if (pl.semantics == kOcv32) {
             hipLaunchKernelGGL(resize_level_ocv32_kernel, dim3((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F),
                                dim3(256), 0, s, P, l);
             continue;
         }
-        // staged tile fits when both ratios are <= 1.25: 256 * 1.25 + 12 bytes <= kRsW words,
-        // 32 * 1.25 + 2 rows <= kRsRows
-        const bool lds = 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h;
+        const bool lds = lds_ok(l);
         if (lds)
             hipLaunchKernelGGL(resize_level_lds_kernel,
                                dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) * xcd_frames(F)),

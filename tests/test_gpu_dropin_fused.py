@@ -116,8 +116,9 @@ def test_pair_stream_record_equals_batched_stream(gpu_ctx):
     frames, K = synth_frames(1280, 720, range(4))
     ps = ops.PairStream(1280, 720, K, nfeatures=2000, ctx=gpu_ctx)
     fs = FrameStream(1280, 720, K, nfeatures=2000, max_frames=4, ctx=gpu_ctx)
-    want = FrameStream.records_numpy(fs.process(torch.from_numpy(frames).cuda()), 3)
+    rec = fs.process(torch.from_numpy(frames).cuda())
     fs.sync()
+    want = FrameStream.records_numpy(rec, 3)
     for p in range(3):
         got = ps.pair(frames[p], frames[p + 1], reuse_prev=p > 0)
         for k in ("R", "t", "E", "n_kp_prev", "n_kp_cur", "n_matches", "n_inliers", "n_good", "ransac_iters", "status",
