@@ -472,15 +472,16 @@ def rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows, K, ctx):
         def step(i):
             s0, k = (i % n_windows) * B, i % S
             fs = fss[k]
-            fs.wait_event(getattr(fs, "_tail_done", None))  # the slot's records were read by its last tail
+            fs.wait_event(getattr(fs, "_tail_done", None))  # the slot's records were read by its last "collective"
             fs.process(pool[s0:s0 + B + 1], recs_t[k], wait_torch=False)
             if with_tail:
                 cur.wait_event(fs.record_event())  # the records are final (before the collective)
+                # stands in for the all-gather: it reads the send buffer, and the library waits only for it
                 wrecs[k][:B * rb].copy_(recs_t[k][:B * rb])
-                tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
                 ev = torch.cuda.Event()
                 ev.record(cur)
                 fs._tail_done = ev
+                tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
 
         for i in range(args.warmup):
             step(i)

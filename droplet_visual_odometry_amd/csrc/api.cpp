@@ -784,34 +784,49 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
             return rc;
     }
     Staging st;
-    int rc = staging(ctx, Staging::round(sizeof(dvo_pair_record)), s->hs, &st);
+    const size_t img_bytes = (size_t)w * h;
+    int rc = staging(ctx, Staging::round(sizeof(dvo_pair_record)) + (reuse_prev ? 1 : 2) * Staging::round(img_bytes),
+                     s->hs, &st);
     if (rc) return rc;
     const int pw = frame_pitch(s);
+    // host frames go through the pinned staging area: one host copy, one asynchronous DMA each
+    auto upload = [&](uint8_t* dst, const uint8_t* img) -> hipError_t {
+        uint8_t* hp = st.take(img_bytes);
+        if (stride == w) {
+            std::memcpy(hp, img, img_bytes);
+        } else {
+            for (int y = 0; y < h; ++y) std::memcpy(hp + (size_t)y * w, img + (size_t)y * stride, w);
+        }
+        return hipMemcpy2DAsync(dst, pw, hp, w, w, h, hipMemcpyHostToDevice, s->hs);
+    };
     const int64_t fst = (int64_t)pw * h;
     const Buffers& b = s->buf;
-    // slot a's features -> slot b's (keypoints, descriptors, count, status)
-    auto move_feats = [&](const dvo_keypoint* k0, const uint8_t* d0, const int32_t* n0, const int32_t* st0,
-                          dvo_keypoint* k1, uint8_t* d1, int32_t* n1, int32_t* st1) -> hipError_t {
-        hipError_t e;
-        if ((e = hipMemcpyAsync(k1, k0, kc * sizeof(dvo_keypoint), hipMemcpyDeviceToDevice, s->hs)) != hipSuccess ||
-            (e = hipMemcpyAsync(d1, d0, kc * 32, hipMemcpyDeviceToDevice, s->hs)) != hipSuccess ||
-            (e = hipMemcpyAsync(n1, n0, sizeof(int32_t), hipMemcpyDeviceToDevice, s->hs)) != hipSuccess)
-            return e;
-        return hipMemcpyAsync(st1, st0, sizeof(int32_t), hipMemcpyDeviceToDevice, s->hs);
+    // the feature arrays of frame 0, frame 1 and the cache (the last current frame's), in 4-byte words
+    FeatSlots fsl{};
+    auto slot = [&](int k, void* kps, void* desc, int32_t* n, int32_t* stt) {
+        fsl.a[k][0] = (uint32_t*)kps;
+        fsl.a[k][1] = (uint32_t*)desc;
+        fsl.a[k][2] = (uint32_t*)n;
+        fsl.a[k][3] = (uint32_t*)stt;
     };
+    slot(0, b.kps, b.desc, b.nkp, b.status);
+    slot(1, b.kps + kc, b.desc + kc * 32, b.nkp + 1, b.status + 1);
+    slot(2, s->fc_kps, s->fc_desc, s->fc_n, s->fc_n + 1);
+    fsl.words[0] = (int)(kc * sizeof(dvo_keypoint) / 4);
+    fsl.words[1] = (int)(kc * 32 / 4);
+    fsl.words[2] = fsl.words[3] = 1;
     if (reuse_prev) {
-        HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, cur_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+        HIP_TRY(upload(s->d_frames, cur_img));
         if ((rc = run_stream(s, s->d_frames, 1, fst, pw, nullptr, true))) return rc;
-        HIP_TRY(move_feats(b.kps, b.desc, b.nkp, b.status, b.kps + kc, b.desc + kc * 32, b.nkp + 1, b.status + 1));
-        HIP_TRY(move_feats(s->fc_kps, s->fc_desc, s->fc_n, s->fc_n + 1, b.kps, b.desc, b.nkp, b.status));
+        // frame 1 <- the new frame's features (frame 0), frame 0 <- the cached previous frame's, and the
+        // cache <- the new frame's (the next pair's previous frame): one launch, element by element
+        HIP_TRY(launch_feature_rotate(fsl, 1, s->hs));
     } else {
-        HIP_TRY(hipMemcpy2DAsync(s->d_frames, pw, prev_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
-        HIP_TRY(hipMemcpy2DAsync(s->d_frames + fst, pw, cur_img, stride, w, h, hipMemcpyHostToDevice, s->hs));
+        HIP_TRY(upload(s->d_frames, prev_img));
+        HIP_TRY(upload(s->d_frames + fst, cur_img));
         if ((rc = run_stream(s, s->d_frames, 2, fst, pw, nullptr, true))) return rc;
+        HIP_TRY(launch_feature_rotate(fsl, 0, s->hs));  // the current frame's features are the next previous
     }
-    // the current frame's features are the next pair's previous frame
-    HIP_TRY(move_feats(b.kps + kc, b.desc + kc * 32, b.nkp + 1, b.status + 1, s->fc_kps, s->fc_desc, s->fc_n,
-                       s->fc_n + 1));
     StreamParams P = params_of(s, s->d_frames, 2, fst, pw);
     const int nqb = ((int)kc + 255) / 256, nst = ((int)kc + 63) / 64;
     int tsplit = 1;

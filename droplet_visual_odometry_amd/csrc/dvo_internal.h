@@ -288,6 +288,14 @@ inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
     if (ev) hipEventRecord(ev[2 * stage + end], s);
 }
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nullptr);
+// dvo_stream_pair's feature bookkeeping in one launch, per 4-byte word i of the frame-0 / frame-1 / cache
+// feature arrays (keypoints, descriptors, count, status): rotate = 1 (frame 0 holds the new current
+// frame): frame 1 <- frame 0, frame 0 <- cache, cache <- frame 0; rotate = 0: cache <- frame 1.
+struct FeatSlots {
+    uint32_t* a[3][4];  // [frame 0, frame 1, cache][kps, desc, count, status]
+    int words[4];
+};
+hipError_t launch_feature_rotate(const FeatSlots& f, int rotate, hipStream_t s);
 // GaussianBlur of every level into Buffers::blur.  On the detection path only when describe_kernel
 // reads a blurred pyramid (describe_blurs() false); otherwise for dvo_stream_get_pyramid(blurred).
 hipError_t launch_blur(const StreamParams& P, hipStream_t s);

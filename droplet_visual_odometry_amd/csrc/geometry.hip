@@ -2292,14 +2292,24 @@ __global__ void pose_tail_kernel(TailArgs a) {
 // carry-out of P_prev / T_abs for the next batch.  The product is not
 // associative in floating point, so the chain stays sequential (bit-identical
 // to the scalar left-to-right 4x4 product); what is parallel is inside a step.
-// Row r of the running pose depends only on row r of the previous one, so
-// lane r (mod 4) keeps its whole row in registers and a step is 16 muls and
-// 12 adds in 4 independent column chains: no cross-lane traffic on the
-// dependency chain.  T_rel is staged through LDS 64 pairs at a time and read
-// one step ahead as wave-uniform broadcasts.
+// Lane 4 r + c (of 16) keeps element (r, c) of the running pose; a step is that
+// element's 4 products and 3 sums, ((t_r0 A_0c + t_r1 A_1c) + t_r2 A_2c) + t_r3 A_3c,
+// with row r's four elements taken from the lane's quad by DPP quad_perm.  The
+// dependency chain of a step is then one quad exchange and 4 dependent f64 ops
+// (round 3 kept a whole row per lane: 28 f64 instructions issued per step).
+// T_rel is staged through LDS 64 pairs at a time and read one step ahead.
+template <int K>
+__device__ __forceinline__ double quad_bcast(double v) {  // lane 4 q + K of the lane's quad
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    constexpr int ctl = K | (K << 2) | (K << 4) | (K << 6);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, ctl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), ctl, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
 __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
-    constexpr int kChunk = 64;
+    constexpr int kChunk = 64, kPer = kChunk * 16 / 64;  // T_rel doubles per lane and chunk
     __shared__ double tr[kChunk * 16];
+    __shared__ double ob[kChunk * 16];  // the chunk's T_abs, stored to global memory coalesced
     const int lane = threadIdx.x;
     int last_ok = -1;
     if (a.rec) {
@@ -2308,48 +2318,51 @@ __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
     }
-    const int r = lane & 3;
-    double t0 = a.tcarry[r * 4 + 0], t1 = a.tcarry[r * 4 + 1], t2 = a.tcarry[r * 4 + 2], t3 = a.tcarry[r * 4 + 3];
+    const int e = lane & 15, c = e & 3;  // lanes 16..63 repeat lanes 0..15
+    double t = a.tcarry[e];
+    // the next chunk's T_rel in flight in registers while this chunk's steps run
+    double nxt[kPer];
+    auto fetch = [&](int p0) {
+        const int n16 = min(kChunk, a.pairs - p0) * 16;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = lane + 64 * k;
+            nxt[k] = i < n16 ? a.T_rel[(int64_t)p0 * 16 + i] : 0.0;
+        }
+    };
+    if (a.pairs > 0) fetch(0);
     for (int p0 = 0; p0 < a.pairs; p0 += kChunk) {
         const int n = min(kChunk, a.pairs - p0);
         __syncthreads();
-        for (int i = lane; i < n * 16; i += 64) tr[i] = a.T_rel[(int64_t)p0 * 16 + i];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) tr[lane + 64 * k] = nxt[k];
         __syncthreads();
-        // software pipeline: step q+1's T_rel is read from LDS while step q computes, so
-        // no LDS latency sits on the dependency chain
-        double A[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) A[k] = tr[k];
-        for (int q = 0; q < n; ++q) {
-            const int qn = min(q + 1, n - 1);
-            double B[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) B[k] = tr[qn * 16 + k];  // the same address in every lane
-            const double u0 = t0 * A[0] + t1 * A[4] + t2 * A[8] + t3 * A[12];
-            const double u1 = t0 * A[1] + t1 * A[5] + t2 * A[9] + t3 * A[13];
-            const double u2 = t0 * A[2] + t1 * A[6] + t2 * A[10] + t3 * A[14];
-            const double u3 = t0 * A[3] + t1 * A[7] + t2 * A[11] + t3 * A[15];
-            t0 = u0;
-            t1 = u1;
-            t2 = u2;
-            t3 = u3;
-            if (lane < 4) {
-                double* o = a.T_abs + (int64_t)(p0 + q) * 16 + r * 4;
-                o[0] = t0;
-                o[1] = t1;
-                o[2] = t2;
-                o[3] = t3;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) A[k] = B[k];
+        if (p0 + kChunk < a.pairs) fetch(p0 + kChunk);
+        // software pipeline, unrolled by two so the two column buffers alternate without moves:
+        // the column of step q + 1 is read from LDS while step q computes
+        auto step = [&](int q, double C0, double C1, double C2, double C3) {
+            const double t0 = quad_bcast<0>(t), t1 = quad_bcast<1>(t), t2 = quad_bcast<2>(t), t3 = quad_bcast<3>(t);
+            t = t0 * C0 + t1 * C1 + t2 * C2 + t3 * C3;
+            ob[q * 16 + e] = t;  // lanes e, e + 16, .. store the same value
+        };
+        double A0 = tr[c], A1 = tr[4 + c], A2 = tr[8 + c], A3 = tr[12 + c];
+        int q = 0;
+        for (; q + 1 < n; q += 2) {
+            const int q1 = q + 1, q2 = min(q + 2, n - 1);
+            const double B0 = tr[q1 * 16 + c], B1 = tr[q1 * 16 + 4 + c], B2 = tr[q1 * 16 + 8 + c],
+                         B3 = tr[q1 * 16 + 12 + c];
+            step(q, A0, A1, A2, A3);
+            A0 = tr[q2 * 16 + c];
+            A1 = tr[q2 * 16 + 4 + c];
+            A2 = tr[q2 * 16 + 8 + c];
+            A3 = tr[q2 * 16 + 12 + c];
+            step(q1, B0, B1, B2, B3);
         }
+        if (q < n) step(q, A0, A1, A2, A3);
+        __syncthreads();
+        for (int i = lane; i < n * 16; i += 64) a.T_abs[(int64_t)p0 * 16 + i] = ob[i];
     }
-    if (lane < 4) {
-        a.tcarry[r * 4 + 0] = t0;
-        a.tcarry[r * 4 + 1] = t1;
-        a.tcarry[r * 4 + 2] = t2;
-        a.tcarry[r * 4 + 3] = t3;
-    }
+    if (lane < 16) a.tcarry[e] = t;
     if (lane == 0 && last_ok >= 0 && a.carry) proj_of(a.K, rec_Rt(a.rec, last_ok), a.carry);
 }
 

@@ -1872,6 +1872,28 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     return hipGetLastError();
 }
 
+namespace {
+__global__ __launch_bounds__(256) void feature_rotate_kernel(FeatSlots f, int rotate) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < f.words[b]; i += gridDim.x * 256) {
+            if (rotate) {
+                const uint32_t cur = f.a[0][b][i], prev = f.a[2][b][i];
+                f.a[1][b][i] = cur;
+                f.a[0][b][i] = prev;
+                f.a[2][b][i] = cur;
+            } else {
+                f.a[2][b][i] = f.a[1][b][i];
+            }
+        }
+}
+}  // namespace
+
+hipError_t launch_feature_rotate(const FeatSlots& f, int rotate, hipStream_t s) {
+    hipLaunchKernelGGL(feature_rotate_kernel, dim3(64), dim3(256), 0, s, f, rotate);
+    return hipGetLastError();
+}
+
 hipError_t launch_test_retain_best(float* d_resp, uint32_t* d_payload, int32_t* d_tmp, int n, int n_points, int depth,
                                    int semantics, int* d_k, hipStream_t s) {
     hipLaunchKernelGGL(test_retain_best_kernel, dim3(1), dim3(kSelNT), 0, s, d_resp, d_payload, d_tmp, n, n_points,

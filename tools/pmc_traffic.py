@@ -61,7 +61,10 @@ def main(fetch, write, sq, calib, dst, batch=1024, rdreq=None):
             e[c] = v
         kernels[k] = e
     doc = {
-        "config": {"width": 1280, "height": 720, "nfeatures": 2000, "batch": int(batch), "streams": 1},
+        # the workload the passes ran (tools/profile_round.sh WL=...): DVO_PMC_CONFIG="width height nfeatures"
+        "config": dict(zip(("width", "height", "nfeatures"),
+                           (int(v) for v in os.environ.get("DVO_PMC_CONFIG", "1280 720 2000").split())),
+                       batch=int(batch), streams=1),
         "unit": "per launch: bytes (FETCH_SIZE/WRITE_SIZE KB x1024, then the width calibration), "
                 "SQ_* instruction counts (wave-level)",
         "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts), mean over dispatches",

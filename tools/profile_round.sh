@@ -15,7 +15,9 @@ tag=$1; part=$2; shift 2
 root=$(pwd)
 out="$root/gpurun_out/prof"
 mkdir -p "$out"
-short="--steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
+# WL: workload flags for every pass (e.g. WL="--width 640 --height 480 --nfeatures 1000"); the merge then
+# needs DVO_PMC_CONFIG="640 480 1000" so bench.py finds the document for that workload
+short="$WL --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
 if [ "$part" = merge ]; then
   python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_calib_rdreq.csv" > /dev/null
   python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512 "$out/${tag}_pmc_rdreq.csv"
