@@ -18,4 +18,7 @@ python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_stall -name '*counte
 timeout -s KILL 170 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES \
   -d /tmp/pmc_${tag}_f64 -o run --output-format csv -- python3 "$root/bench.py" $short "$@" > "$out/${tag}_pmc_f64.log" 2>&1
 python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_f64 -name '*counter_collection.csv') "$out/${tag}_pmc_f64.csv" > /dev/null
+# Durand-Kerner per pass: the f64 pass's per-dispatch counts against a counter-free kernel trace of the same bench
+timeout -k 10 170 rocprofv3 --kernel-trace -d /tmp/pmc_${tag}_kt -o run --output-format csv -- python3 "$root/bench.py" $short "$@" > "$out/${tag}_dk_trace.log" 2>&1
+python3 "$root/tools/dk_passes.py" $(find /tmp/pmc_${tag}_f64 -name '*counter_collection.csv') $(find /tmp/pmc_${tag}_kt -name '*kernel_trace.csv') "$out/${tag}_dk_passes.json" > "$out/${tag}_dk_passes.txt"
 rm -rf /tmp/pmc_${tag}_*
