@@ -33,13 +33,58 @@ __constant__ int8_t c_pattern[256 * 4] = {
 // ICAngles u_max for halfPatchSize 15 (orb.cpp computeKeyPoints): cvRound of
 // sqrt(225 - v^2) for v <= 11, then the symmetry fix-up; pinned by a test.
 constexpr int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-// the same table as 16 nibbles: umax(v) = (kUmaxPacked >> 4v) & 15, no memory access
-constexpr unsigned long long umax_packed() {
-    unsigned long long p = 0;
-    for (int i = 0; i < 16; ++i) p |= (unsigned long long)c_umax[i] << (4 * i);
-    return p;
+// describe_kernel's ICAngles disk membership per lane: lane (h, c) = (lane >> 5, lane & 31) takes
+// column u = c - 15 of rows v = 2 it + h - 15, it = 0..15; bit it set when (u, v) lies in the disk
+// (|u| <= umax(|v|), v <= 15, c < 31).  Keypoint independent: one load instead of ~100 VALU.
+struct IcMasks {
+    uint16_t m[64];
+};
+constexpr IcMasks ic_masks() {
+    IcMasks r{};
+    for (int lane = 0; lane < 64; ++lane) {
+        const int u = (lane & 31) - 15, au = u < 0 ? -u : u;
+        unsigned bits = 0;
+        for (int it = 0; it < 16; ++it) {
+            const int v = 2 * it + (lane >> 5) - 15, av = v < 0 ? -v : v;
+            bits |= (unsigned)(v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av]) << it;
+        }
+        r.m[lane] = (uint16_t)bits;
+    }
+    return r;
 }
-constexpr unsigned long long kUmaxPacked = umax_packed();
+__constant__ IcMasks c_icmask = ic_masks();
+// DVO_IC_DOT4: the same moments from whole LDS words, two lanes per window row (words 0..4 and
+// 5..9 of the row's 9; word 9 weighs nothing), v_dot4_u32_u8 against per-(alignment, row, word)
+// weight words: byte weight u + 15 (in [0, 30]) inside the disk, 0 outside, and a 0/1 word for the
+// plain sum.  m10 = sum (u + 15) I - 15 sum I, m01 = v sum I per row; integer sums, so the same
+// m10 / m01 as the per-pixel loop.  o = (kx - 15) & 3: the keypoint column's byte offset in
+// the row's first word minus 15 (the window starts at the aligned (kx - 15) & ~3).
+#ifndef DVO_IC_DOT4
+#define DVO_IC_DOT4 1
+#endif
+struct IcTable {
+    uint32_t w[4][32][10][2];  // [o][row][word] = {weights u + 15, ones}; row 31 is the idle lanes' zeros
+};
+constexpr IcTable ic_table() {
+    IcTable t{};
+    for (int o = 0; o < 4; ++o)
+        for (int r = 0; r < 31; ++r)
+            for (int w = 0; w < 9; ++w) {
+                uint32_t wu = 0, w1 = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int u = 4 * w + b - 15 - o, v = r - 15;
+                    const int au = u < 0 ? -u : u, av = v < 0 ? -v : v;
+                    if (au <= c_umax[av]) {
+                        wu |= (uint32_t)(u + 15) << (8 * b);
+                        w1 |= 1u << (8 * b);
+                    }
+                }
+                t.w[o][r][w][0] = wu;
+                t.w[o][r][w][1] = w1;
+            }
+    return t;
+}
+__constant__ IcTable c_ictab = ic_table();
 
 // FAST 16-pixel Bresenham circle (dx, dy), fast.cpp makeOffsets.
 constexpr int kCdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -1607,16 +1652,10 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const uint32_t*>(c_pattern)[q * 64 + lane];
     // ICAngles disk membership of this lane's 16 samples (u = column, v = row): keypoint independent
+#if !DVO_IC_DOT4
     const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
-    const int au = u < 0 ? -u : u;
-    uint32_t inbits = 0;
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int v = 2 * it + (lane >> 5) - 15;  // rows -15..16; row 16 unused
-        const int av = v < 0 ? -v : v;
-        const int um = (int)(kUmaxPacked >> (4 * (av > 15 ? 15 : av))) & 15;
-        inbits |= (uint32_t)(v <= 15 && (lane & 31) < 31 && au <= um) << it;
-    }
+    const uint32_t inbits = c_icmask.m[lane];
+#endif
     // keypoint (level, index, key) of this wave's 4 slots, keys requested together
     int lv[kDKW], ix[kDKW];
     uint32_t keys[kDKW];
@@ -1735,6 +1774,25 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #endif
         __builtin_amdgcn_wave_barrier();
         // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
+#if DVO_IC_DOT4
+        int m10, m01;
+        {
+            const int r = lane >> 1, hh = lane & 1;  // window row (31: lanes 62, 63, zero weights), word half
+            const uint32_t* rowp = reinterpret_cast<const uint32_t*>(&icw[wv][0][0]) + r * (kICW / 4) + 5 * hh;
+            const uint2* tp = reinterpret_cast<const uint2*>(&c_ictab.w[(kx - 15) & 3][r][5 * hh][0]);
+            uint32_t dU = 0, d1 = 0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {  // word 9 (the next row's first) has zero weights
+                const uint32_t I4 = rowp[q];
+                const uint2 t = tp[q];
+                dU = __builtin_amdgcn_udot4(I4, t.x, dU, false);
+                d1 = __builtin_amdgcn_udot4(I4, t.y, d1, false);
+            }
+            m10 = (int)dU - 15 * (int)d1;
+            m01 = (r - 15) * (int)d1;
+        }
+        (void)ai;
+#else
         const uint8_t* col = &icw[wv][0][0] + (kx - ai) + u;
         int sI = 0, m01 = 0;
 #pragma unroll
@@ -1745,6 +1803,7 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
             m01 += v * I;
         }
         int m10 = u * sI;
+#endif
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             m10 += __shfl_xor(m10, o);
