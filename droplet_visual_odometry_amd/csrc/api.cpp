@@ -907,7 +907,7 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
     const LevelGeom& G = s->plan.L[level];
     if (cap < G.w * G.h) return fail(ctx, DVO_ECAP, "capacity too small");
     HIP_TRY(hipStreamSynchronize(s->hs));
-    if (blurred && describe_blurs()) {
+    if (blurred) {
         // the detection path blurs only the descriptor windows (describe_kernel): the whole blurred
         // pyramid is recomputed here from the last call's frames, which must still be alive
         HIP_TRY(launch_blur(params_of(s, s->last_frames, s->last_nframes, s->last_fstride, s->last_pitch), s->hs));

@@ -296,10 +296,9 @@ struct FeatSlots {
     int words[4];
 };
 hipError_t launch_feature_rotate(const FeatSlots& f, int rotate, hipStream_t s);
-// GaussianBlur of every level into Buffers::blur.  On the detection path only when describe_kernel
-// reads a blurred pyramid (describe_blurs() false); otherwise for dvo_stream_get_pyramid(blurred).
+// GaussianBlur of every level into Buffers::blur, for dvo_stream_get_pyramid(blurred): the
+// detection path blurs only the pixels describe_kernel samples.
 hipError_t launch_blur(const StreamParams& P, hipStream_t s);
-bool describe_blurs();
 // tsplit > 1 splits every pair's train stages over tsplit workgroups (one pair alone fills the chip)
 hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, hipEvent_t* ev = nullptr, int tsplit = 1);
 // one_round: a single RANSAC round over every hypothesis up to maxIters on the 16-lane Durand-Kerner

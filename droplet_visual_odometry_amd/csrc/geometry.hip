@@ -2071,16 +2071,15 @@ __global__ __launch_bounds__(64) void pose_decompose_kernel(GeomArgs g, int pair
 }
 
 // One thread per (point, rotation c in {0, 1}): decompositions c ([R_c|t]) and c + 2 ([R_c|-t])
-// from ONE triangulation (DVO_POSE_MIRROR).  Their DLT matrices differ only in column 3, negated
+// from ONE triangulation (round 4: recoverPose 1.20 -> 0.62 ms one-stream,
+// profiles/r04m_ab_pose_mirror.txt; tests/test_pose_mirror.py checks the identity on the
+// oracle's Jacobi SVD).  Their DLT matrices differ only in column 3, negated
 // (row 0-1 entries are zeros, t's entries are exact negations: t + 0.0 and 0.0 - t), and the
 // Jacobi SVD keeps that mirror exactly: a rotation pairing column 3 with another sees -p, hence
 // -s with the same c, and every later value is the exact negation (IEEE rounding is symmetric;
 // only the signs of exact zeros can differ).  So the c + 2 null vector is sigma (X0, X1, X2, -X3),
 // sigma = +-1, and its tests are those of c with X2 X3, q = X / X3 and z negated.  A zero X3
 // (q infinite: a zero's sign would matter) or a zero component of t takes the c + 2 SVD itself.
-#ifndef DVO_POSE_MIRROR
-#define DVO_POSE_MIRROR 1
-#endif
 __device__ __forceinline__ bool pose_tests(const double (&X)[4], const double* Pl, double dist, bool mirror) {
     if (!mirror) {
         bool ok = X[2] * X[3] > 0;
@@ -2105,9 +2104,8 @@ __global__ __launch_bounds__(kPNT) void pose_count_kernel(GeomArgs g) {
     if (!cnt[0]) return;
     const int m = pair_m(g, p);
     const int w = blockIdx.x * kPNT + threadIdx.x;
-    constexpr int kPer = DVO_POSE_MIRROR ? 2 : 4;  // threads per point
-    if ((int)blockIdx.x * kPNT >= kPer * m) return;
-    const int c = w & (kPer - 1), i = w / kPer;
+    if ((int)blockIdx.x * kPNT >= 2 * m) return;
+    const int c = w & 1, i = w >> 1;
     bool ok = false, ok2 = false;  // decompositions c and (mirror) c + 2
     if (i < m) {
         const double P0[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
@@ -2124,35 +2122,25 @@ __global__ __launch_bounds__(kPNT) void pose_count_kernel(GeomArgs g) {
         if (g.mask_in) mv &= g.mask_in[mi];  // bitwise_and(mask, mask_c)
         ok = mv != 0;
         if (g.pose_mask) g.pose_mask[mi * 4 + c] = mv;
-        if (kPer == 2) {
-            if (X[3] != 0 && Pl[3] != 0 && Pl[7] != 0 && Pl[11] != 0) {
-                ok2 = pose_tests(X, Pl, g.dist_thresh, true);
-            } else {  // the c + 2 decomposition's own triangulation
+        if (X[3] != 0 && Pl[3] != 0 && Pl[7] != 0 && Pl[11] != 0) {
+            ok2 = pose_tests(X, Pl, g.dist_thresh, true);
+        } else {  // the c + 2 decomposition's own triangulation
 #pragma unroll
-                for (int k = 0; k < 12; ++k) Pl[k] = Pc[24 + k];
-                triangulate_one(P0, Pl, pt[0], pt[1], pt[2], pt[3], X);
-                ok2 = pose_tests(X, Pl, g.dist_thresh, false);
-            }
-            uint8_t mv2 = ok2 ? 255 : 0;
-            if (g.mask_in) mv2 &= g.mask_in[mi];
-            ok2 = mv2 != 0;
-            if (g.pose_mask) g.pose_mask[mi * 4 + c + 2] = mv2;
+            for (int k = 0; k < 12; ++k) Pl[k] = Pc[24 + k];
+            triangulate_one(P0, Pl, pt[0], pt[1], pt[2], pt[3], X);
+            ok2 = pose_tests(X, Pl, g.dist_thresh, false);
         }
+        uint8_t mv2 = ok2 ? 255 : 0;
+        if (g.mask_in) mv2 &= g.mask_in[mi];
+        ok2 = mv2 != 0;
+        if (g.pose_mask) g.pose_mask[mi * 4 + c + 2] = mv2;
     }
-    if (kPer == 4) {
-        const unsigned long long bal = __ballot(ok);  // lane l holds decomposition l & 3
-        if ((threadIdx.x & 63) < 4) {
-            const int n = __popcll(bal & (0x1111111111111111ull << (threadIdx.x & 3)));
-            if (n) atomicAdd(&cnt[1 + (threadIdx.x & 3)], n);
-        }
-    } else {
-        const unsigned long long b0 = __ballot(ok), b2 = __ballot(ok2);  // lane l: decompositions l & 1, (l & 1) + 2
-        const int lane = threadIdx.x & 63;
-        if (lane < 4) {
-            const unsigned long long bal = lane < 2 ? b0 : b2;
-            const int n = __popcll(bal & (0x5555555555555555ull << (lane & 1)));
-            if (n) atomicAdd(&cnt[1 + lane], n);
-        }
+    const unsigned long long b0 = __ballot(ok), b2 = __ballot(ok2);  // lane l: decompositions l & 1, (l & 1) + 2
+    const int lane = threadIdx.x & 63;
+    if (lane < 4) {
+        const unsigned long long bal = lane < 2 ? b0 : b2;
+        const int n = __popcll(bal & (0x5555555555555555ull << (lane & 1)));
+        if (n) atomicAdd(&cnt[1 + lane], n);
     }
 }
 
@@ -2440,7 +2428,7 @@ hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStr
     }
     if (stages & kStagePose) {
         hipLaunchKernelGGL(pose_decompose_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs);
-        hipLaunchKernelGGL(pose_count_kernel, dim3((unsigned)(((DVO_POSE_MIRROR ? 2 : 4) * g.pts_stride + kPNT - 1) / kPNT), pairs), dim3(kPNT), 0,
+        hipLaunchKernelGGL(pose_count_kernel, dim3((unsigned)((2 * g.pts_stride + kPNT - 1) / kPNT), pairs), dim3(kPNT), 0,
                            s, g);
         hipLaunchKernelGGL(pose_pick_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, pairs);
     }

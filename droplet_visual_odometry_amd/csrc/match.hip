@@ -42,28 +42,20 @@ namespace {
 // trains through one L2.
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
-typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kMWaves = 4, kMQB = 64 * kMWaves, kMStage = 64;
 constexpr int kKeyBase = 1 << 20;     // 256 * 4096
 
-// Operand format.  DVO_MATCH_FP4=1 (default): v_mfma_scale_f32_32x32x64_f8f6f4
-// on e2m1 (fp4) operands, +-1.0 per descriptor bit (a nibble each: 32 bits of
-// a descriptor word = one 16-byte chunk), the train side's block scale 2^12, so
-// the f32 accumulator is D = -4096 s exactly (integers < 2^21); keys are formed
-// in f32 (exact below 2^24) and compared as the bit patterns of non-negative
-// floats (ordered like the values).  Twice the i8 form's K per clock and half
-// its LDS bytes per train.  DVO_MATCH_FP4=0: the i8 form
-// (v_mfma_i32_32x32x32_i8, +-64 bytes, 16 chunks of 16 bits per train).
-#ifndef DVO_MATCH_FP4
-#define DVO_MATCH_FP4 1
-#endif
-#if DVO_MATCH_FP4
+// Operand format: v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 (fp4) operands,
+// +-1.0 per descriptor bit (a nibble each: 32 bits of a descriptor word = one
+// 16-byte chunk), the train side's block scale 2^12, so the f32 accumulator is
+// D = -4096 s exactly (integers < 2^21); keys are formed in f32 (exact below
+// 2^24) and compared as the bit patterns of non-negative floats (ordered like
+// the values).  Twice the K per clock of the i8 form (v_mfma_i32_32x32x32_i8 on
+// +-64 bytes, round 3's first matcher) and half its LDS bytes per train.
 constexpr int kMChunks = 8;   // 16-byte operand chunks per train
 constexpr int kMKs = 4;       // MFMAs per 32x32 block
-constexpr int kChunkBits = 32;
 typedef v16f acc_t;
-constexpr int kKeyNone = 0x7F000000;  // bits of ~1.7e38f: above every key, not a NaN
 // 32 descriptor bits to 32 e2m1 nibbles (a permutation of the bit order that A
 // and B share, so the dot product is unchanged): nibble-spread of byte k is
 // L | H << 4, L / H the byte's low / high nibble spread to bytes by
@@ -88,34 +80,8 @@ __device__ __forceinline__ acc_t mfma_chunk(v4i a, v4i b, acc_t c) {
 }
 // key bits of accumulator element a plus the exact integer c (both as f32)
 __device__ __forceinline__ int key_add(float a, float c) { return __float_as_int(a + c); }
-__device__ __forceinline__ float key_const(int c) { return (float)c; }
-typedef float kconst_t;
 __device__ __forceinline__ int key_value(int kbits) { return (int)__int_as_float(kbits); }
-#else
-constexpr int kMChunks = 16;
-constexpr int kMKs = 8;
-constexpr int kChunkBits = 16;
-typedef v16i acc_t;
-constexpr int kKeyNone = 0x40000000;  // > any valid key (< 2^22), < 0x7F7F7F7F
-// 16 descriptor bits (chunk c = bits 16c .. 16c+15 = packed bytes 2c, 2c+1) to
-// 16 bytes, byte j from bit j: (nibble * 0x204081) & 0x01010101 spreads a
-// nibble's bit i to byte i; base ^ (spread << 7) flips 0x40 <-> 0xC0 (+-64).
-// Query side base 0xC0C0C0C0 (set -> +64), train side 0x40404040 (set -> -64).
-__device__ __forceinline__ v4i expand_chunk(uint32_t bits, uint32_t base) {
-    v4i r;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = (int)(base ^ ((((bits >> (4 * k)) & 0xFu) * 0x00204081u & 0x01010101u) << 7));
-    return r;
-}
-constexpr uint32_t kExpQ = 0xC0C0C0C0u, kExpT = 0x40404040u;
-__device__ __forceinline__ acc_t mfma_chunk(v4i a, v4i b, acc_t c) {
-    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ int key_add(int a, int c) { return a + c; }
-__device__ __forceinline__ int key_const(int c) { return c; }
-typedef int kconst_t;
-__device__ __forceinline__ int key_value(int kbits) { return kbits; }
-#endif
+constexpr int kKeyNone = 0x7F000000;  // bits of ~1.7e38f: above every key, not a NaN
 constexpr int kChunkMask = kMChunks - 1;
 __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 8191); }
 
@@ -124,16 +90,11 @@ __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 
 template <bool kFull>
 __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][kMKs], int (&best)[2][16], int t0,
                                          int nt, int r, int h, int rowb, int nq) {
-#ifndef DVO_MATCH_HOIST
-#define DVO_MATCH_HOIST 1
-#endif
-#if DVO_MATCH_FP4
     const float rbf = (float)rowb;  // + goff below: exact, loop-invariant (hoisted into registers)
-#endif
 #pragma unroll 1
     for (int tt = 0; tt < kMStage / 32; ++tt) {
         const int j = t0 + 32 * tt + r;
-        const kconst_t cf = key_const(j < nt ? kKeyBase + j : (DVO_MATCH_FP4 ? (1 << 30) : kKeyNone));
+        const float cf = (float)(j < nt ? kKeyBase + j : (1 << 30));
         acc_t acc0 = {}, acc1 = {};
 #pragma unroll
         for (int ks = 0; ks < kMKs; ++ks) {
@@ -142,24 +103,12 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
             acc1 = mfma_chunk(A[1][ks], B, acc1);
         }
         int cm = 0x7FFFFFFF;
-#if !DVO_MATCH_FP4
-        int rb = rowb;
-        asm volatile("" : "+v"(rb));  // keep rowb + goff out of 32 hoisted registers: one v_add3 per element
-#endif
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int goff = (g & 3) + 8 * (g >> 2);
             best[0][g] = min(best[0][g], key_add(acc0[g], cf));
             best[1][g] = min(best[1][g], key_add(acc1[g], cf));
-#if DVO_MATCH_FP4 && !DVO_MATCH_HOIST
-            float rb = rbf;
-            asm volatile("" : "+v"(rb));  // not hoisted: 32 fewer live registers, one more add per element
-            int k0 = key_add(acc0[g], rb + (float)goff), k1 = key_add(acc1[g], rb + (float)(32 + goff));
-#elif DVO_MATCH_FP4
             int k0 = key_add(acc0[g], rbf + (float)goff), k1 = key_add(acc1[g], rbf + (float)(32 + goff));
-#else
-            int k0 = acc0[g] + rb + goff, k1 = acc1[g] + rb + (32 + goff);
-#endif
             if (!kFull) {
                 k0 = rowb - kKeyBase + goff < nq ? k0 : kKeyNone;
                 k1 = rowb - kKeyBase + 32 + goff < nq ? k1 : kKeyNone;
@@ -220,7 +169,7 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
 #pragma unroll
         for (int ks = 0; ks < kMKs; ++ks) {  // chunk 2 ks + h; a zero fragment past nq
             const int ch = 2 * ks + h;
-            const uint32_t bits = kChunkBits == 32 ? wd[ch] : wd[ch >> 1] >> (16 * (ch & 1));
+            const uint32_t bits = wd[ch];
             A[s2][ks] = q < nq ? expand_chunk(bits, kExpQ) : (v4i){0, 0, 0, 0};
         }
 #pragma unroll
@@ -241,7 +190,7 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
 #pragma unroll
         for (int c = 0; c < kPer; ++c) {
             const int ch = kPer * qd + c;
-            const uint32_t bits = kChunkBits == 32 ? (c == 0 ? v.x : v.y) : (c < 2 ? v.x : v.y) >> (16 * (c & 1));
+            const uint32_t bits = c == 0 ? v.x : v.y;
             bt[b][tr * kMChunks + (ch ^ (tr & kChunkMask))] = in ? expand_chunk(bits, kExpT) : (v4i){0, 0, 0, 0};
         }
         if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;

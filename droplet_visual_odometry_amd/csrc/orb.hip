@@ -7,8 +7,8 @@
 // Stages (DESIGN.md §4 lists the roofline of each):
 //   resize_level_kernel   INTER_LINEAR_EXACT 8-bit fixed point, level l-1 -> l
 //   blur_kernel           GaussianBlur 7x7 sigma 2, 8-bit fixed-point separable, of every level:
-//                         only for dvo_stream_get_pyramid(blurred) when describe_kernel
-//                         blurs its own windows (DVO_DESCRIBE_BLUR, the default)
+//                         only for dvo_stream_get_pyramid(blurred); describe_kernel blurs
+//                         the pixels its own windows sample
 //   fast_strip_kernel     FAST-9/16 + strict 3x3 NMS + border cut + per-row
 //                         compaction, one column strip of one level per workgroup
 //   select_fast_kernel    KeyPointsFilter::retainBest(2n) by FAST score: exact
@@ -33,35 +33,13 @@ __constant__ int8_t c_pattern[256 * 4] = {
 // ICAngles u_max for halfPatchSize 15 (orb.cpp computeKeyPoints): cvRound of
 // sqrt(225 - v^2) for v <= 11, then the symmetry fix-up; pinned by a test.
 constexpr int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
-// describe_kernel's ICAngles disk membership per lane: lane (h, c) = (lane >> 5, lane & 31) takes
-// column u = c - 15 of rows v = 2 it + h - 15, it = 0..15; bit it set when (u, v) lies in the disk
-// (|u| <= umax(|v|), v <= 15, c < 31).  Keypoint independent: one load instead of ~100 VALU.
-struct IcMasks {
-    uint16_t m[64];
-};
-constexpr IcMasks ic_masks() {
-    IcMasks r{};
-    for (int lane = 0; lane < 64; ++lane) {
-        const int u = (lane & 31) - 15, au = u < 0 ? -u : u;
-        unsigned bits = 0;
-        for (int it = 0; it < 16; ++it) {
-            const int v = 2 * it + (lane >> 5) - 15, av = v < 0 ? -v : v;
-            bits |= (unsigned)(v <= 15 && (lane & 31) < 31 && au <= c_umax[av > 15 ? 15 : av]) << it;
-        }
-        r.m[lane] = (uint16_t)bits;
-    }
-    return r;
-}
-__constant__ IcMasks c_icmask = ic_masks();
-// DVO_IC_DOT4: the same moments from whole LDS words, two lanes per window row (words 0..4 and
-// 5..9 of the row's 9; word 9 weighs nothing), v_dot4_u32_u8 against per-(alignment, row, word)
-// weight words: byte weight u + 15 (in [0, 30]) inside the disk, 0 outside, and a 0/1 word for the
-// plain sum.  m10 = sum (u + 15) I - 15 sum I, m01 = v sum I per row; integer sums, so the same
-// m10 / m01 as the per-pixel loop.  o = (kx - 15) & 3: the keypoint column's byte offset in
+// describe_kernel's ICAngles moments from whole LDS words, two lanes per window row (words 0..4
+// and 5..9 of the row's 9; word 9 weighs nothing), v_dot4_u32_u8 against per-(alignment, row,
+// word) weight words: byte weight u + 15 (in [0, 30]) inside the disk |u| <= umax(|v|), 0
+// outside, and a 0/1 word for the plain sum.  m10 = sum (u + 15) I - 15 sum I, m01 = v sum I per
+// row; integer sums, so the same m10 / m01 as orb.cpp's per-pixel loop (round 4: 6.36 -> 5.67 ms
+// one-stream, profiles/r04n_ab_describe_ic.txt).  o = (kx - 15) & 3: the keypoint column's byte offset in
 // the row's first word minus 15 (the window starts at the aligned (kx - 15) & ~3).
-#ifndef DVO_IC_DOT4
-#define DVO_IC_DOT4 1
-#endif
 struct IcTable {
     uint32_t w[4][32][10][2];  // [o][row][word] = {weights u + 15, ones}; row 31 is the idle lanes' zeros
 };
@@ -1525,8 +1503,8 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
 // keypoints per wave, the loads of all of them requested first.  Reading a blurred pyramid: 1 73.0 K,
 // 2 73.6 K, 4 72.3 K frames/s (profiles/r02z_ab_describe_dkw.txt); blurring the windows here
-// (DVO_DESCRIBE_BLUR, 16 raw rows per lane and keypoint): 1 74.8 K (51 VGPRs), 2 74.3 K (119 VGPRs),
-// against 73.2 K for the separate blur pass (profiles/r03o_ab_describe_blur.txt)
+// (16 raw rows per lane and keypoint): 1 74.8 K (51 VGPRs), 2 74.3 K (119 VGPRs), against 73.2 K
+// for the separate blur pass (profiles/r03o_ab_describe_blur.txt)
 #ifndef DVO_DKW
 #define DVO_DKW 1
 #endif
@@ -1534,39 +1512,27 @@ constexpr int kDKW = DVO_DKW;          // keypoints per wave
 constexpr int kDKB = 4 * kDKW;         // keypoints per workgroup
 constexpr int kICW = 36, kICR = 36;    // IC window: rows ky-15 .. ky+15 (+ padding) x 9 aligned words
 
-// DVO_DESCRIBE_BLUR: the GaussianBlur of the 39 x 44 window is computed here from
-// the raw level instead of being read from a blurred copy of the pyramid written
-// by blur_kernel (which then does not run on the detection path).  Lane
-// (s, wc) = (lane / 13, lane % 13), s < 4 (lanes 52..63 idle): raw word wc of the
-// window row span [a0 - 4, a0 + 48) (words 0 and 12 are the horizontal halo), 10
-// output rows 10 s .. 10 s + 9 of the patch from 16 raw rows, the vertical
-// 7-tap over a rolling window of u16 pairs and the horizontal taps from the
-// neighbouring lanes (wave_shr / wave_shl), with blur_wave's arithmetic and
-// rounding rule (half to even below w & ~3, half up in the w % 4 tail).
-// Keypoints lie >= 31 pixels from every border and the window reaches 22, so
-// no reflection is needed.
-#ifndef DVO_DESCRIBE_BLUR
-#define DVO_DESCRIBE_BLUR 1
-#endif
+// The GaussianBlur of the pixels the descriptor samples is computed here from the
+// raw level instead of being read from a blurred copy of the pyramid (blur_kernel,
+// which does not run on the detection path; round 3, and FAST writing the blurred
+// tiles in round 4 lost 9 %, profiles/r04l_ab_fast_blur.txt).  A band's lanes hold
+// raw words of the window row span around the keypoint (a halo word each side), 8
+// output rows from 14 raw rows, the vertical 7-tap over a rolling window of u16
+// pairs and the horizontal taps from the neighbouring lanes (wave_shr /
+// wave_shl), with blur_wave's arithmetic and rounding rule (half to even below
+// w & ~3, half up in the w % 4 tail).  Keypoints lie >= 31 pixels from every
+// border and the window reaches 22, so no reflection is needed.
 // Only the pixels the rotated pattern can sample are blurred: pattern points lie within
 // r = 18.385 of the centre (|x|, |y| <= 13), so a sample rounds to |dy| <= 18 and, in row dy,
 // |dx| <= floor(sqrt(r^2 - (|dy| - 1/2)^2) + 1/2) (r for dy = 0): 6, 8, 10, .. 18 .. 6 (equal to
 // the extents of cvRound over a 2e5-step angle sweep).  Five bands of 8 patch rows
 // (dy = -18 + 8s .. -11 + 8s) take 11, 12, 12, 12 and 9 lanes (the band's words at its largest
 // |dx| for any keypoint alignment, plus a halo word each side): 56 lanes, 8 rows each, where the
-// full 39 x 44 window needed 52 lanes x 10 rows.  DVO_DESCRIBE_DISK=0: the full window.
-#ifndef DVO_DESCRIBE_DISK
-#define DVO_DESCRIBE_DISK 1
-#endif
-#if DVO_DESCRIBE_DISK
+// full 39 x 44 window needed 52 lanes x 10 rows.
 constexpr int kDBRows = 8, kDBSeg = 5, kDBRaw = kDBRows + 6;  // output rows per band, bands, raw rows
 constexpr int kDBRow0 = 1;                                     // patch row of band 0's first row (dy = -18)
 constexpr int kDBBase[kDBSeg + 1] = {0, 11, 23, 35, 47, 56};    // first lane of each band
 constexpr int kDBHalfW[kDBSeg] = {15, 18, 18, 18, 12};          // largest |dx| in the band
-#else
-constexpr int kDBRows = 10, kDBSeg = 4, kDBRaw = kDBRows + 6;  // output rows per lane segment, segments, raw rows
-constexpr int kDBRow0 = 0;
-#endif
 
 __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw], uint8_t* patch_slot, int s, int wc,
                                                    bool he, bool st) {
@@ -1620,6 +1586,22 @@ __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw]
     }
 }
 
+// Sum over the wave by DPP (quad swaps, row shifts, row broadcasts; invalid source lanes read 0),
+// the total read from lane 63: six DPP adds instead of six ds_bpermute rounds.
+template <int kCtl, int kRowMask = 0xF>
+__device__ __forceinline__ int dpp_or_zero(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, kCtl, kRowMask, 0xF, false);
+}
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += dpp_or_zero<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_or_zero<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_or_zero<0x114>(v);  // row_shr:4
+    v += dpp_or_zero<0x118>(v);  // row_shr:8  -> lane 15 of each row: the row's sum
+    v += dpp_or_zero<0x142>(v);  // row_bcast:15
+    v += dpp_or_zero<0x143>(v);  // row_bcast:31 -> lane 63: the wave's sum
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     __shared__ __attribute__((aligned(16))) uint8_t patch[kDKB][kDPH + 2][kDPW];  // + 2 padding rows
     __shared__ __attribute__((aligned(16))) uint8_t icw[4][kICR][kICW];
@@ -1652,10 +1634,6 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const uint32_t*>(c_pattern)[q * 64 + lane];
     // ICAngles disk membership of this lane's 16 samples (u = column, v = row): keypoint independent
-#if !DVO_IC_DOT4
-    const int u = (lane & 31) - 15;  // lanes 0..30 -> u in [-15, 15]
-    const uint32_t inbits = c_icmask.m[lane];
-#endif
     // keypoint (level, index, key) of this wave's 4 slots, keys requested together
     int lv[kDKW], ix[kDKW];
     uint32_t keys[kDKW];
@@ -1676,10 +1654,8 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     }
     // ---- phase 1: every keypoint of this wave requests both windows first (one load latency
     // covers the wave's kDKW keypoints), then each is staged in LDS and gets its IC angle
-    constexpr int kIW = 31 * (kICW / 4), kPW = kDPH * (kDPW / 4);
-#if DVO_DESCRIBE_BLUR
+    constexpr int kIW = 31 * (kICW / 4);
     uint32_t ivs[kDKW][5], pvs[kDKW][kDBRaw];
-#if DVO_DESCRIBE_DISK
     int db_s = 0;
 #pragma unroll
     for (int q = 1; q < kDBSeg; ++q) db_s += lane >= kDBBase[q];
@@ -1687,13 +1663,6 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     const int db_hw = db_s == 0 ? kDBHalfW[0] : db_s == 4 ? kDBHalfW[4] : kDBHalfW[1];
     const bool db_st = db_k >= 1 && db_k <= kDBBase[db_s + 1] - kDBBase[db_s] - 2;  // not a band halo word
     int db_wcs[kDKW];
-#else
-    const int db_s = lane / 13, db_wc = lane - 13 * db_s;  // lanes >= 52: segment 4 (loads in range, no store)
-    constexpr bool db_st = true;
-#endif
-#else
-    uint32_t ivs[kDKW][5], pvs[kDKW][7];
-#endif
 #pragma unroll
     for (int kk = 0; kk < kDKW; ++kk) {  // slots past nk read the clamped last keypoint (unused)
         const int l = lv[kk];
@@ -1707,42 +1676,23 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         const int ai = (kx - 15) & ~3;
         const int step = level_pitch(P, l);
         const uint8_t* img = level_ptr(P, f, l) + (int64_t)(ky - 15) * step + ai;
-#ifdef DVO_EXP_SKIP_BLUR  // timing experiment: sample the unblurred level (descriptors still discriminate)
-        const int bpitch = step;
-        const uint8_t* bl = level_ptr(P, f, l) + (int64_t)(cyb - kDPR) * bpitch + a0;
-#else
-        const int bpitch = G.bpitch;
-        const uint8_t* bl = blur_ptr(P, f, l) + (int64_t)(cyb - kDPR) * bpitch + a0;
-#endif
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const int ec = min(64 * t + lane, kIW - 1);
             const int rc = ec / (kICW / 4), wc = ec - rc * (kICW / 4);
             ivs[kk][t] = *reinterpret_cast<const uint32_t*>(img + (int64_t)rc * step + 4 * wc);
         }
-#if DVO_DESCRIBE_BLUR
         {  // raw rows cyb - 22 + 10 s .. + 15 of word db_wc of [a0 - 4, a0 + 48)
             const int sr = min(db_s, kDBSeg - 1);
-#if DVO_DESCRIBE_DISK
             // the band's first word: the one left of the word holding cx - halfwidth (raw word
             // index ((x - a0) >> 2) + 1); <= 12 for every lane of the band
             const int db_wc = min(((cxb - db_hw - a0) >> 2) + db_k, 12);
             db_wcs[kk] = db_wc;
-#endif
             const uint8_t* rw = level_ptr(P, f, l) + (int64_t)(cyb - kDPR - 3 + kDBRow0 + kDBRows * sr) * step +
                                 a0 - 4 + 4 * db_wc;
 #pragma unroll
             for (int t = 0; t < kDBRaw; ++t) pvs[kk][t] = *reinterpret_cast<const uint32_t*>(rw + (int64_t)t * step);
-            (void)bl;
         }
-#else
-#pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            const int ec = min(64 * t + lane, kPW - 1);
-            const int rc = ec / (kDPW / 4), wc = ec - rc * (kDPW / 4);
-            pvs[kk][t] = *reinterpret_cast<const uint32_t*>(bl + (int64_t)rc * bpitch + 4 * wc);
-        }
-#endif
     }
 #pragma unroll
     for (int kk = 0; kk < kDKW; ++kk) {
@@ -1762,19 +1712,11 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
-#if DVO_DESCRIBE_BLUR
-#if DVO_DESCRIBE_DISK
         const int db_wc = db_wcs[kk];
-#endif
         describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc,
                            a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w, db_st);
-#else
-#pragma unroll
-        for (int t = 0; t < 7; ++t) reinterpret_cast<uint32_t*>(&patch[slot][0][0])[64 * t + lane] = pvs[kk][t];
-#endif
         __builtin_amdgcn_wave_barrier();
         // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
-#if DVO_IC_DOT4
         int m10, m01;
         {
             const int r = lane >> 1, hh = lane & 1;  // window row (31: lanes 62, 63, zero weights), word half
@@ -1792,23 +1734,8 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
             m01 = (r - 15) * (int)d1;
         }
         (void)ai;
-#else
-        const uint8_t* col = &icw[wv][0][0] + (kx - ai) + u;
-        int sI = 0, m01 = 0;
-#pragma unroll
-        for (int it = 0; it < 16; ++it) {
-            const int v = 2 * it + (lane >> 5) - 15;
-            const int I = (inbits >> it) & 1 ? (int)col[(v + 15) * kICW] : 0;
-            sI += I;
-            m01 += v * I;
-        }
-        int m10 = u * sI;
-#endif
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            m10 += __shfl_xor(m10, o);
-            m01 += __shfl_xor(m01, o);
-        }
+        m10 = wave_sum_dpp(m10);  // integer sums: the order does not matter
+        m01 = wave_sum_dpp(m01);
         if (lane == 0) {
             const float angle = fast_atan2((float)m01, (float)m10);
             s_ang[slot] = angle;
@@ -1877,9 +1804,9 @@ hipError_t launch_blur(const StreamParams& P, hipStream_t s) {
     return hipGetLastError();
 }
 
-bool describe_blurs() { return DVO_DESCRIBE_BLUR != 0; }
 
-hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
+namespace {
+hipError_t launch_orb_frames(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     const Plan& pl = P.plan;
     const int F = P.nframes;
     mark(ev, 0, 0, s);
@@ -1903,9 +1830,6 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     }
     mark(ev, 0, 1, s);
     mark(ev, 1, 0, s);
-#if !defined(DVO_EXP_SKIP_BLUR) && !DVO_DESCRIBE_BLUR  // describe blurs its own windows (DVO_DESCRIBE_BLUR)
-    hipLaunchKernelGGL(blur_kernel, dim3(pl.total_tiles * xcd_frames(F)), dim3(256), 0, s, P);
-#endif
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
@@ -1929,6 +1853,54 @@ hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
     hipLaunchKernelGGL(describe_kernel, dim3(xcd_frames(F) * ((pl.kp_cap + kDKB - 1) / kDKB)), dim3(256), 0, s, P);
     mark(ev, 4, 1, s);
     return hipGetLastError();
+}
+
+// Frames [f0, f0 + n) of P as a batch of their own: every per-frame buffer the detection
+// kernels index by frame advanced by f0 frames.
+StreamParams frame_group(const StreamParams& P, int f0, int n) {
+    StreamParams Q = P;
+    const Plan& pl = P.plan;
+    const int64_t f = f0;
+    Q.nframes = n;
+    Q.frames = P.frames + f * P.frame_stride;
+    Q.buf.pyr += f * pl.pyr_stride;
+    Q.buf.blur += f * pl.blur_stride;
+    Q.buf.band_cnt += f * pl.total_bands * kBandRows;
+    Q.buf.band_cand += f * pl.band_cand_stride;
+    Q.buf.cand += f * pl.cand_stride;
+    Q.buf.resp += f * pl.cand_stride;
+    Q.buf.sel_tmp += f * 2 * pl.cand_stride;
+    Q.buf.cnt1 += f * kMaxLevels;
+    Q.buf.cnt2 += f * kMaxLevels;
+    Q.buf.kps += f * pl.kp_cap;
+    Q.buf.desc += f * pl.kp_cap * 32;
+    Q.buf.nkp += f;
+    Q.buf.status += f;
+    return Q;
+}
+}  // namespace
+
+// DVO_ORB_GROUP > 0: a batch's detection runs pyramid -> FAST -> selections -> Harris -> describe
+// over groups of that many frames in turn, so a group's pyramid (2.85 MB per 1280x720 frame) can
+// still sit in the Infinity Cache when Harris and describe re-read it.
+// 0: every stage over the whole batch.  Stage events then bracket the whole detection.
+#ifndef DVO_ORB_GROUP
+#define DVO_ORB_GROUP 0
+#endif
+hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
+    const int F = P.nframes, grp = DVO_ORB_GROUP;
+    if (grp <= 0 || F <= grp) return launch_orb_frames(P, s, ev);
+    mark(ev, 0, 0, s);
+    for (int f0 = 0; f0 < F; f0 += grp) {
+        const hipError_t e = launch_orb_frames(frame_group(P, f0, std::min(grp, F - f0)), s, nullptr);
+        if (e != hipSuccess) return e;
+    }
+    mark(ev, 0, 1, s);
+    for (int st = 1; st <= 4; ++st) {
+        mark(ev, st, 0, s);
+        mark(ev, st, 1, s);
+    }
+    return hipSuccess;
 }
 
 namespace {

@@ -1,5 +1,5 @@
 """describe_kernel blurs only the pixels a rotated rBRIEF pattern point can
-round to (csrc/orb.hip DVO_DESCRIBE_DISK; orb.cpp computeOrbDescriptors,
+round to (csrc/orb.hip kDBRows / kDBBase / kDBHalfW; orb.cpp computeOrbDescriptors,
 reached from visual_odometry_v3.py:373).  Checked here on the host, from the
 constants in orb.hip: every (dy, dx) that cvRound of the float32 rotation of a
 pattern point reaches, over a fine angle sweep and by the closed-form bound,
@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _consts():
     src = open(os.path.join(ROOT, "droplet_visual_odometry_amd", "csrc", "orb.hip")).read()
-    block = src[src.index("#if DVO_DESCRIBE_DISK"):]
+    block = src[src.index("constexpr int kDBRows"):]
     rows = int(re.search(r"kDBRows = (\d+), kDBSeg = (\d+)", block).group(1))
     seg = int(re.search(r"kDBRows = (\d+), kDBSeg = (\d+)", block).group(2))
     row0 = int(re.search(r"kDBRow0 = (\d+)", block).group(1))

@@ -192,3 +192,34 @@ def test_detect_noise_frame_long_lists(gpu_ctx, oracle_mod):
     ko, do = oracle_mod.detect_and_compute(img, 2000)
     np.testing.assert_array_equal(kg.view(np.uint8), ko.view(np.uint8))
     np.testing.assert_array_equal(dg, do)
+
+
+def test_large_batch_equals_small_batches(gpu_ctx):
+    """A 200-frame batch (detection over frame groups when DVO_ORB_GROUP is set, csrc/orb.hip
+    launch_orb) gives every frame the features and every pair the record that 2-frame batches of
+    the same frames give."""
+    import torch
+    from droplet_visual_odometry_amd.stream import FrameStream
+    W, H, N, F = 320, 240, 300, 200
+    frames, K = synth_frames(W, H, range(F))
+    big = FrameStream(W, H, K, nfeatures=N, max_frames=F, ctx=gpu_ctx)
+    dev = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
+    rec = big.process(dev)
+    big.sync()
+    recs = FrameStream.records_numpy(rec, F - 1)
+    small = FrameStream(W, H, K, nfeatures=N, max_frames=2, ctx=gpu_ctx)
+    for i in (0, 62, 63, 64, 127, 128, 190, 198):
+        r2 = small.process(dev[i:i + 2])
+        small.sync()
+        for k in (0, 1):
+            kb, db = big.features(i + k)
+            ks, ds = small.features(k)
+            np.testing.assert_array_equal(kb.view(np.uint8), ks.view(np.uint8), err_msg=f"frame {i + k}")
+            np.testing.assert_array_equal(db, ds, err_msg=f"frame {i + k}")
+        rs = FrameStream.records_numpy(r2, 1)[0]
+        for name in recs.dtype.names:
+            if name not in ("pad0", "reserved"):
+                np.testing.assert_array_equal(recs[i][name], rs[name], err_msg=f"pair {i} {name}")
+    big.close()
+    small.close()
+    del dev
