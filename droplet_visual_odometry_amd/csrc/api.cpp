@@ -81,6 +81,7 @@ struct dvo_stream {
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
     std::vector<std::vector<hipEvent_t>> ev_pending;
+    std::vector<int> ev_groups;  // per pending table: detection frame groups (orb_groups), 0 = none
     std::vector<std::vector<hipEvent_t>> ev_free;
     double stage_ms[DVO_NSTAGES] = {0};
     int prof_calls = 0;
@@ -479,17 +480,19 @@ dvo_orb_params default_orb(int nfeatures) {
     return o;
 }
 
-int acquire_events(dvo_stream* s, hipEvent_t** ev) {
+// A table: 2 events per stage, then 2 x 5 per detection frame group (launch_orb's group_ev).
+int acquire_events(dvo_stream* s, int groups, hipEvent_t** ev) {
     dvo_ctx* ctx = s->ctx;
     std::vector<hipEvent_t> e;
     if (!s->ev_free.empty()) {
         e = std::move(s->ev_free.back());
         s->ev_free.pop_back();
     } else {
-        e.resize(2 * DVO_NSTAGES);
+        e.resize(2 * DVO_NSTAGES + 10 * orb_groups(s->cfg.max_frames));
         for (auto& x : e) HIP_TRY(hipEventCreate(&x));
     }
     s->ev_pending.push_back(std::move(e));
+    s->ev_groups.push_back(groups);
     *ev = s->ev_pending.back().data();
     return DVO_OK;
 }
@@ -497,16 +500,26 @@ int acquire_events(dvo_stream* s, hipEvent_t** ev) {
 // Drain completed event tables into the per-stage totals (blocks on the last).
 int collect_events(dvo_stream* s) {
     dvo_ctx* ctx = s->ctx;
-    for (auto& e : s->ev_pending) {
+    for (size_t i = 0; i < s->ev_pending.size(); ++i) {
+        auto& e = s->ev_pending[i];
+        const int groups = s->ev_groups[i];
         HIP_TRY(hipEventSynchronize(e[2 * DVO_NSTAGES - 1]));
         for (int st = 0; st < DVO_NSTAGES; ++st) {
             float ms = 0;
-            if (hipEventElapsedTime(&ms, e[2 * st], e[2 * st + 1]) == hipSuccess) s->stage_ms[st] += ms;
+            if (st <= 4 && groups > 0) {  // detection in frame groups: the stage's time summed over them
+                for (int g = 0; g < groups; ++g)
+                    if (hipEventElapsedTime(&ms, e[2 * DVO_NSTAGES + 10 * g + 2 * st],
+                                            e[2 * DVO_NSTAGES + 10 * g + 2 * st + 1]) == hipSuccess)
+                        s->stage_ms[st] += ms;
+            } else if (hipEventElapsedTime(&ms, e[2 * st], e[2 * st + 1]) == hipSuccess) {
+                s->stage_ms[st] += ms;
+            }
         }
         s->prof_calls++;
         s->ev_free.push_back(std::move(e));
     }
     s->ev_pending.clear();
+    s->ev_groups.clear();
     return DVO_OK;
 }
 
@@ -517,12 +530,13 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     P.pair_step = pair_step;
     const int pairs = stream_pairs(P);
     hipEvent_t* ev = nullptr;
+    const int groups = orb_groups(n);
     if (s->profiling && !detect_only && pairs >= 1) {
-        int rc = acquire_events(s, &ev);
+        int rc = acquire_events(s, groups, &ev);
         if (rc) return rc;
     }
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
-    HIP_TRY(launch_orb(P, s->hs, ev));
+    HIP_TRY(launch_orb(P, s->hs, ev, ev && groups ? ev + 2 * DVO_NSTAGES : nullptr));
     s->last_nframes = n;
     s->last_frames = d_frames;
     s->last_fstride = fstride;

@@ -771,7 +771,7 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
         const int r1 = min(r0 + kBandRows, h - kBorder);
         const int nrows = r1 - r0;
         const int item = G.band_base + b * G.ntx + c;
-        // ---- window: carried rows 0..7, new rows 8..23; score rows 0, 1 carried (tile 0: zero)
+        // ---- window: carried rows 0..7, new rows 8..kFtRows-1; score rows 0, 1 carried (tile 0: zero)
 #pragma unroll
         for (int k = 0; k < kFtCarryR; ++k) {
             const int q = threadIdx.x + k * kFastNT;
@@ -1880,25 +1880,27 @@ StreamParams frame_group(const StreamParams& P, int f0, int n) {
 }
 }  // namespace
 
-// DVO_ORB_GROUP > 0: a batch's detection runs pyramid -> FAST -> selections -> Harris -> describe
-// over groups of that many frames in turn, so a group's pyramid (2.85 MB per 1280x720 frame) can
-// still sit in the Infinity Cache when Harris and describe re-read it.
-// 0: every stage over the whole batch.  Stage events then bracket the whole detection.
+// DVO_ORB_GROUP > 0: a batch of more than that many frames runs its detection (pyramid -> FAST ->
+// selections -> Harris -> describe) over ceil(F / DVO_ORB_GROUP) groups of equal size (+-1) in turn
+// (the group's pyramid is still in the caches when Harris and describe
+// re-read it).  Two-stream bench, whole batch 87.6-88.2 K; groups of 64 -8 %, 128 -2 %, 256
+// +0.8 to +1.5 %, 512 / 1024 +-0 (profiles/r04o_ab_describe_sincos_groups.txt, r04p_ab*.txt,
+// r04q_ab_orb_groups.txt); one stream alone is slower (small launches), two overlap better.  Stage
+// events: one table of 2 x 5 per group (orb_groups), summed per stage.
 #ifndef DVO_ORB_GROUP
-#define DVO_ORB_GROUP 0
+#define DVO_ORB_GROUP 256
 #endif
-hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev) {
-    const int F = P.nframes, grp = DVO_ORB_GROUP;
-    if (grp <= 0 || F <= grp) return launch_orb_frames(P, s, ev);
-    mark(ev, 0, 0, s);
-    for (int f0 = 0; f0 < F; f0 += grp) {
-        const hipError_t e = launch_orb_frames(frame_group(P, f0, std::min(grp, F - f0)), s, nullptr);
+int orb_groups(int nframes) {
+    const int grp = DVO_ORB_GROUP;
+    return grp > 0 && nframes > grp ? (nframes + grp - 1) / grp : 0;
+}
+hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev, hipEvent_t* group_ev) {
+    const int F = P.nframes, G = orb_groups(F);
+    if (G == 0) return launch_orb_frames(P, s, ev);
+    for (int g = 0; g < G; ++g) {
+        const int f0 = (int)((int64_t)F * g / G), f1 = (int)((int64_t)F * (g + 1) / G);
+        const hipError_t e = launch_orb_frames(frame_group(P, f0, f1 - f0), s, group_ev ? group_ev + 10 * g : nullptr);
         if (e != hipSuccess) return e;
-    }
-    mark(ev, 0, 1, s);
-    for (int st = 1; st <= 4; ++st) {
-        mark(ev, st, 0, s);
-        mark(ev, st, 1, s);
     }
     return hipSuccess;
 }

@@ -195,12 +195,12 @@ def test_detect_noise_frame_long_lists(gpu_ctx, oracle_mod):
 
 
 def test_large_batch_equals_small_batches(gpu_ctx):
-    """A 200-frame batch (detection over frame groups when DVO_ORB_GROUP is set, csrc/orb.hip
-    launch_orb) gives every frame the features and every pair the record that 2-frame batches of
-    the same frames give."""
+    """A 300-frame batch (detection in two frame groups of 150, csrc/orb.hip launch_orb,
+    DVO_ORB_GROUP 256) gives every frame the features and every pair the record that 2-frame
+    batches of the same frames give, across the group boundary too (pair 149)."""
     import torch
     from droplet_visual_odometry_amd.stream import FrameStream
-    W, H, N, F = 320, 240, 300, 200
+    W, H, N, F = 320, 240, 300, 300
     frames, K = synth_frames(W, H, range(F))
     big = FrameStream(W, H, K, nfeatures=N, max_frames=F, ctx=gpu_ctx)
     dev = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
@@ -208,7 +208,7 @@ def test_large_batch_equals_small_batches(gpu_ctx):
     big.sync()
     recs = FrameStream.records_numpy(rec, F - 1)
     small = FrameStream(W, H, K, nfeatures=N, max_frames=2, ctx=gpu_ctx)
-    for i in (0, 62, 63, 64, 127, 128, 190, 198):
+    for i in (0, 62, 148, 149, 150, 151, 255, 256, 298):
         r2 = small.process(dev[i:i + 2])
         small.sync()
         for k in (0, 1):

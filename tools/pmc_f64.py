@@ -14,7 +14,10 @@ F64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64"
 def main(src, dst, batch=512, launches=2, width=1280, height=720, nfeatures=2000):
     batch, launches = int(batch), int(launches)
     kernels = {}
-    for r in csv.DictReader(open(src)):
+    rows = list(csv.DictReader(open(src)))
+    # launches: normalize_kernel runs once per batch launch (falls back to the argument)
+    launches = next((int(r["dispatches"]) for r in rows if r["kernel"] == "normalize_kernel"), launches)
+    for r in rows:
         d = int(r["dispatches"])
         per = d / launches  # dispatches per batch launch; the CSV holds means per dispatch
         k = {c.replace("SQ_INSTS_VALU_", "").lower(): float(r.get(c) or 0.0) * per for c in F64}

@@ -21,9 +21,15 @@ KERNEL_WIDTHS = {
 
 
 def load(path, counters):
+    """Per kernel: its counters per batch launch = the mean per dispatch x dispatches per launch
+    (a kernel can run several times per batch: pyramid levels, RANSAC rounds and passes, frame
+    groups of the detection).  Launches = the dispatches of normalize_kernel (once per batch)."""
+    rows = list(csv.DictReader(open(path)))
+    launches = next((float(r["dispatches"]) for r in rows if r["kernel"] == "normalize_kernel"), 2.0)
     out = {}
-    for r in csv.DictReader(open(path)):
-        out[r["kernel"]] = {c: float(r[c]) for c in counters if c in r and r[c] != ""}
+    for r in rows:
+        per = float(r.get("dispatches") or launches) / launches
+        out[r["kernel"]] = {c: float(r[c]) * per for c in counters if c in r and r[c] != ""}
     return out
 
 
@@ -67,7 +73,8 @@ def main(fetch, write, sq, calib, dst, batch=1024, rdreq=None):
                        batch=int(batch), streams=1),
         "unit": "per launch: bytes (FETCH_SIZE/WRITE_SIZE KB x1024, then the width calibration), "
                 "SQ_* instruction counts (wave-level)",
-        "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts), mean over dispatches",
+        "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts); per batch launch: the "
+                "mean over dispatches x dispatches per launch",
         "calibration": os.path.basename(calib),
         "read_bytes": "32 n32 + 64 n64 + 128 n128 from the TCC_EA0_RDREQ_*B pass" if rq else "FETCH_SIZE x width factor",
         "kernels": kernels,
