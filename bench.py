@@ -71,9 +71,10 @@ def parse():
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--nfeatures", type=int, default=2000)
-    ap.add_argument("--batch", type=int, default=2048,
+    ap.add_argument("--batch", type=int, default=3072,
                     help="new frames per step (pairs per step); two streams, 1280x720: 1024 68.7 K frames/s, "
-                         "1536 70.3 K, 2048 71.0 K, 3072 72.2 K (profiles/r02r_batch_sweep.txt)")
+                         "1536 70.3 K, 2048 71.0 K, 3072 72.2 K (profiles/r02r_batch_sweep.txt); round 4 tree: "
+                         "2048 90.3-90.4 K, 3072 91.4 K, 4096 91.5 K, 3 streams 83.4 K (profiles/r04u_sweep.txt)")
     ap.add_argument("--max-iters", type=int, default=1000)
     ap.add_argument("--pool", type=int, default=0, help="distinct frames rendered per rank (default 2*batch+1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0 = skip)")

@@ -1229,6 +1229,15 @@ __device__ int retain_best_block(const A& a, int n, int npoints, int depth, int3
 #define DVO_SEL_NT 128  // measured: 128 threads 0.81 ms, 256 0.82, 512 1.06, 1024 2.17 (select + Harris, 513 frames)
 #endif
 constexpr int kSelNT = DVO_SEL_NT;
+// select_fast's level-0 blocks (a 1280x720 frame keeps ~15 K FAST corners there, the other levels a
+// few thousand): each quickselect partition step scans the range NT at a time between barriers.  Level
+// 0 in its own launch at 256 threads: two-stream 89.1-89.4 -> 90.3-90.5 K (192: 90.2-90.4, 512: +0.6 %,
+// 1024: -2.4 %; profiles/r04s_ab_bounds_select.txt, r04t_ab_select_level0.txt); alone it is slower
+// (select + Harris 3.73 -> 4.18 ms), beside the other stream the separate launch interleaves better.
+#ifndef DVO_SEL_NT0
+#define DVO_SEL_NT0 256
+#endif
+constexpr int kSelNT0 = DVO_SEL_NT0;
 // Batches of a few frames (the per-call drop-in surface: one frame) are latency-bound:
 // fewer, wider partition chunks.  Drop-in pairs/s at 1280x720 (tools/ab_dropin.sh):
 // 128 threads 429, 256 441, 512 452, 1024 447.
@@ -1247,8 +1256,8 @@ constexpr int kSelLdsCap = 8192;
 constexpr bool kSelLdsCall = DVO_SEL_LDS_CALL != 0;
 
 template <int NT, bool kLds>
-__global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P) {
-    const int l = blockIdx.x, f = blockIdx.y;
+__global__ __launch_bounds__(NT) void select_fast_kernel(StreamParams P, int l0) {
+    const int l = l0 + blockIdx.x, f = blockIdx.y;
     if (l >= P.plan.nlevels) return;
     const LevelGeom& G = P.plan.L[l];
     __shared__ int lds[64];
@@ -1839,9 +1848,13 @@ hipError_t launch_orb_frames(const StreamParams& P, hipStream_t s, hipEvent_t* e
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     if (F <= kSelCallFrames)
-        hipLaunchKernelGGL((select_fast_kernel<kSelNTCall, kSelLdsCall>), dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P);
-    else
-        hipLaunchKernelGGL((select_fast_kernel<kSelNT, false>), dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P);
+        hipLaunchKernelGGL((select_fast_kernel<kSelNTCall, kSelLdsCall>), dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s, P, 0);
+    else if (kSelNT0 != kSelNT) {  // level 0 (the longest lists) on wider blocks, the other levels as before
+        hipLaunchKernelGGL((select_fast_kernel<kSelNT0, false>), dim3(1, F), dim3(kSelNT0), 0, s, P, 0);
+        hipLaunchKernelGGL((select_fast_kernel<kSelNT, false>), dim3(pl.nlevels - 1, F), dim3(kSelNT), 0, s, P, 1);
+    } else {
+        hipLaunchKernelGGL((select_fast_kernel<kSelNT, false>), dim3(pl.nlevels, F), dim3(kSelNT), 0, s, P, 0);
+    }
     hipLaunchKernelGGL(harris_kernel, dim3(harris_blocks_x(pl), pl.nlevels, F), dim3(256), 0, s, P);
     if (F <= kSelCallFrames)
         hipLaunchKernelGGL((select_harris_kernel<kSelNTCall, kSelLdsCall>), dim3(pl.nlevels, F), dim3(kSelNTCall), 0, s,
