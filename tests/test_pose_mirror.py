@@ -1,4 +1,4 @@
-"""recoverPose's [R|t] / [R|-t] mirror (csrc/geometry.hip pose_count_kernel, DVO_POSE_MIRROR),
+"""recoverPose's [R|t] / [R|-t] mirror (csrc/geometry.hip pose_count_kernel),
 checked on the host with the oracle's own triangulatePoints (oracle/geometry.cpp, the same
 Jacobi SVD restatement the device compiles): triangulating against [R|-t] gives exactly
 sigma (X0, X1, X2, -X3) of the [R|t] result (sigma = +-1; IEEE rounding is symmetric, so the
