@@ -1,0 +1,7 @@
+#!/bin/bash
+# default C3 bench line with every leg and the C2 / C5 lines.
+set -e
+mkdir -p gpurun_out/prof
+timeout -k 10 600 python3 -u bench.py > gpurun_out/prof/r04zz_bench_default.json 2> gpurun_out/prof/r04zz_bench_default.err
+timeout -k 10 400 python3 -u bench.py --width 640 --height 480 --nfeatures 1000 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 > gpurun_out/prof/r04zz_bench_640x480_n1000.json 2> gpurun_out/prof/r04zz_bench_640x480_n1000.err
+timeout -k 10 500 python3 -u bench.py --width 1920 --height 1080 --nfeatures 4000 --max-iters 4096 --batch 1024 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 > gpurun_out/prof/r04zz_bench_1920x1080_n4000_it4096_b1024.json 2> gpurun_out/prof/r04zz_bench_1920x1080_n4000_it4096_b1024.err
