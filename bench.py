@@ -225,18 +225,27 @@ def main():
     # the other schedules of the same workload, on the GPU (never `value`)
     i_last = args.warmup + args.steps - 1
     legs = {}
+    def leg(name, fn, *a):
+        # a leg that fails (e.g. out of device memory at an unusual batch) is reported, never the whole line
+        try:
+            legs[name] = fn(*a)
+        except Exception as e:  # noqa: BLE001
+            legs[name] = {"error": f"{type(e).__name__}: {e}"}
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
     if not args.no_ref_equivalent:
-        legs["reference_equivalent"] = ref_equivalent_leg(args, pool, corners, scene.K, ctx, value,
-                                                          recs, (i_last % n_windows) * B)
+        leg("reference_equivalent", ref_equivalent_leg, args, pool, corners, scene.K, ctx, value, recs,
+            (i_last % n_windows) * B)
     if not args.no_host_fed:
         for f in fss:
             f.set_profiling(False)
-        legs["host_fed"] = host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, value)
+        leg("host_fed", host_fed_leg, args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, value)
     if args.tail_world > 1:
         for f in fss:
             f.set_profiling(False)
-        legs[f"rank0_tail_world{args.tail_world}"] = rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows,
-                                                                    scene.K, ctx)
+        leg(f"rank0_tail_world{args.tail_world}", rank0_tail_leg, args, pool, fss, recs_t, corners, n_windows,
+            scene.K, ctx)
 
     cpu = None
     pose_check = None
@@ -244,7 +253,7 @@ def main():
     if args.cpu_seconds > 0:
         cpu, ref = cpu_baseline(pool, scene.K, N, args.max_iters, args.cpu_seconds,
                                 ref_equivalent=not args.no_ref_equivalent)
-        if "reference_equivalent" in legs and cpu.get("reference_equivalent"):
+        if "value" in legs.get("reference_equivalent", {}) and cpu.get("reference_equivalent"):
             re = legs["reference_equivalent"]
             re["cpu_value"] = cpu["reference_equivalent"]["value"]
             re["speedup_vs_cpu_same_mode"] = round(re["value"] / max(re["cpu_value"], 1e-9), 1)
@@ -320,11 +329,14 @@ def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, s
     tensors are gathered from the same device pool before timing.  Its
     records must equal the streaming schedule's byte for byte (detection is
     a function of the frame), which is checked on the streaming run's last
-    window."""
+    window.  Steps carry min(batch, 1024) pairs (2 x that many frames per
+    stream, beside the streaming run's streams, which stay allocated: a
+    stream holds ~16 MB of worst-case candidate and RANSAC buffers per frame)."""
     import torch
     from droplet_visual_odometry_amd.stream import FrameStream
     from droplet_visual_odometry_amd.synth import MARKER_LEN
-    W, H, N, B, S = args.width, args.height, args.nfeatures, args.batch, max(1, args.streams)
+    W, H, N, S = args.width, args.height, args.nfeatures, max(1, args.streams)
+    B = min(args.batch, 1024)
     n_windows = max(1, (len(pool) - 1) // B)
     dev = pool.device
     pp = [pool.index_select(0, torch.tensor([w * B + p + j for p in range(B) for j in (0, 1)], device=dev))
@@ -358,11 +370,15 @@ def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, s
         step(args.warmup + i)
     sync_all()
     dt = time.perf_counter() - t0
-    # the streaming run's last window through the paired schedule: identical records
-    w = stream_first_pair // B
-    fss[0].process_pairs(pp[w], recs[0], wait_torch=False)
+    # the streaming run's last window (its first B pairs) through the paired schedule: identical records
+    chk = pool.index_select(0, torch.tensor([stream_first_pair + p + j for p in range(B) for j in (0, 1)],
+                                            device=dev)).contiguous()
+    fss[0].process_pairs(chk, recs[0], wait_torch=True)  # chk is written on torch's stream
     fss[0].sync()
-    same = bool(np.array_equal(FrameStream.records_numpy(recs[0], B).view(np.uint8), stream_recs.view(np.uint8)))
+    # every field the pair path defines (`reserved` carries pose-tail state of whichever window ran last)
+    got = FrameStream.records_numpy(recs[0], B)
+    differing = [k for k in got.dtype.names if not np.array_equal(got[k], stream_recs[:B][k])]
+    same = not [k for k in differing if k not in ("reserved", "pad0")]
     for f in fss:
         f.close()
     del pp, fss, recs
@@ -370,7 +386,7 @@ def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, s
     value = B * args.steps / dt
     return {"value": round(value, 2), "unit": "frames/s", "ms_per_step": round(1e3 * dt / args.steps, 3),
             "frames_detected_per_step": 2 * B, "pairs_per_step": B, "vs_streaming": round(value / stream_value, 4),
-            "records_identical_to_streaming": same,
+            "records_identical_to_streaming": same, "record_fields_differing": differing,
             "schedule": "reference-equivalent: both frames of every pair detected (v3:387-392), 2B detections "
                         "per B pairs, two batches in flight; value counts pairs (= new frames of the stream)"}
 
