@@ -983,23 +983,11 @@ __global__ __launch_bounds__(256) void normalize_kernel(GeomArgs g) {
 // [0, min(64, niters)) and round 2 everything left, [64, niters)
 // (kRansacBounds): the result is the sequential loop's, bit for bit.
 constexpr int kSolveNT = 64;
-// Wave issue priority of the RANSAC solver kernels (s_setprio, 0..3).  The other stream's ORB
-// kernels share the SIMDs with these long, latency-bound waves; a higher priority lets a solver
-// wave issue first whenever it is ready, and the throughput-bound ORB waves take the rest.
-#ifndef DVO_RANSAC_PRIO
-#define DVO_RANSAC_PRIO 0
-#endif
-__device__ __forceinline__ void dk_priority() {
-    if constexpr (DVO_RANSAC_PRIO > 0) __builtin_amdgcn_s_setprio(DVO_RANSAC_PRIO);
-}
 #ifndef DVO_SCORE_CHUNK
 #define DVO_SCORE_CHUNK 256  // points per LDS chunk: smaller chunks, more resident blocks (measured)
 #endif
 #ifndef DVO_SCORE_HYPS_CALL
 #define DVO_SCORE_HYPS_CALL 2  // drop-in pairs/s (profiles/r02z_ab_dropin_score_hyps.txt): 1 620, 2 626, 4 611, 16 610
-#endif
-#ifndef DVO_SCORE_F32
-#define DVO_SCORE_F32 1  // single-precision decision with the f64 test for the undecided (SampsonF32)
 #endif
 constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 // Deferred f64 Sampson tests per score block: the (model, point) pairs the
@@ -1007,18 +995,12 @@ constexpr int kScoreNT = 256, kScoreHyps = 16, kScoreChunk = DVO_SCORE_CHUNK;
 // stream the chunks, and the whole block runs their f64 tests once, after the
 // last chunk (one latency round trip per block instead of one per wave-chunk
 // that met an undecided point).  A full list falls back to the inline test.
-#ifndef DVO_SCORE_DEFER
-#define DVO_SCORE_DEFER 1
-#endif
 constexpr int kScoreUnd = 1024;
 // Early exit of a model that cannot matter: the replay changes state only at a count above
 // max(maxgood, 4) of the rounds before (RANSACPointSetRegistrator::run's test, ptsetreg.cpp), so
 // once a model's count so far plus its deferred tests plus the points not yet scored is <= that
 // bound, its final count is too, and it stops being scored (the partial count it stores is <= the
 // bound as well: the replay cannot tell the difference).  Round 2 starts from round 1's maxgood.
-#ifndef DVO_SCORE_BAIL
-#define DVO_SCORE_BAIL 1
-#endif
 constexpr int kScoreHypsCall = DVO_SCORE_HYPS_CALL;
 
 // getSubset (ptsetreg.cpp) for the round's hypotheses [h0, h1) of one pair,
@@ -1232,7 +1214,6 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
 
 // Stage A of every hypothesis of the round (one thread each).
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
-    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
@@ -1309,7 +1290,6 @@ __global__ void dk_stats_kernel(int round, int nwaves) {
 #endif
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
-    dk_priority();
     // pass 0: items [0, dk_ctl[1]) of the round's work list; pass k > 0: dk_list[k - 1][0, dk_ctl[1 + k])
     const int total = g.dk_ctl[1 + pass];
     if ((int)blockIdx.x * kDkNT >= total) return;
@@ -1500,7 +1480,6 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
 
 // Stage C of every hypothesis of the round: models and their count.
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
-    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
@@ -1582,7 +1561,6 @@ __global__ __launch_bounds__(64) void ransac_stage_c_row_kernel(GeomArgs g) {
 // so that its few blocks spread over more CUs (fewer models per wave in sequence).
 template <int HYPS>
 __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
-    dk_priority();
     const int p = blockIdx.y;
     const RansacState& S = g.rs[p];
     const int hb = S.h0 + blockIdx.x * HYPS;
@@ -1590,22 +1568,14 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
     const int hn = min(HYPS, S.h1 - hb);
     const int m = S.m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#if !DVO_SCORE_F32
-    __shared__ double s_pts[kScoreChunk * 4];
-    __shared__ double s_E[HYPS * 10 * 9];
-#endif
     __shared__ int s_pref[HYPS + 1];
     __shared__ int s_cnt[HYPS * 10];
-#if DVO_SCORE_F32
     __shared__ float4 s_ptf[kScoreChunk];
     __shared__ float s_sf[HYPS * 10][12];  // SampsonF32 of each model: e[9], mk, ok
     __shared__ int s_moff[HYPS * 10];      // the model's offset in g.models (the f64 test)
-#if DVO_SCORE_DEFER
     __shared__ uint32_t s_und[kScoreUnd];  // deferred f64 tests: model << 16 | point, ~0u = void slot
     __shared__ int s_nund;
     __shared__ int s_pend[HYPS * 10];      // deferred tests per model (possible inliers not yet counted)
-#endif
-#endif
     const int64_t hbase = (int64_t)p * g.hyp_cap + hb;
     static_assert(HYPS < 64, "one wave prefixes the model counts; lane hn (< 64) writes the total");
     if (tid < 64) {  // model counts of the block's hypotheses: one load each, a wave prefix sum
@@ -1618,28 +1588,15 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         }
         if (tid <= hn) s_pref[tid] = x - c;
     }
-#if DVO_SCORE_F32 && DVO_SCORE_DEFER
     if (tid == 0) s_nund = 0;
-#endif
     __syncthreads();
     const int T = s_pref[hn];
-#if !DVO_SCORE_F32
-    for (int e = tid; e < T * 9; e += kScoreNT) {
-        const int mi = e / 9, k = e - mi * 9;
-        int h = 0;
-        while (h + 1 < hn && s_pref[h + 1] <= mi) ++h;
-        s_E[e] = g.models[(hbase + h) * 90 + (mi - s_pref[h]) * 9 + k];
-    }
-#endif
     for (int e = tid; e < T; e += kScoreNT) s_cnt[e] = 0;
-#if DVO_SCORE_F32 && DVO_SCORE_DEFER
     for (int e = tid; e < T; e += kScoreNT) s_pend[e] = 0;
-#endif
     const int bail = max(S.maxgood, 4);  // a final count <= bail never changes the replay
     const double thr = g.threshold / ((g.fx + g.fy) / 2);
     const float t = (float)(thr * thr);
     const bool fast_ok = t >= FLT_MIN;  // the division-free test needs t normal
-#if DVO_SCORE_F32
     for (int e = tid; e < T; e += kScoreNT) {  // once per model, not per chunk
         int h = 0;
         while (h + 1 < hn && s_pref[h + 1] <= e) ++h;
@@ -1654,28 +1611,20 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         s_sf[e][9] = sf.mk;
         s_sf[e][10] = sf.ok ? 1.f : 0.f;
     }
-#endif
     const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
     for (int c0 = 0; c0 < m; c0 += kScoreChunk) {
         const int cn = min(kScoreChunk, m - c0);
         __syncthreads();
-#if !DVO_SCORE_F32
-        for (int e = tid; e < cn * 4; e += kScoreNT) s_pts[e] = npts[(int64_t)c0 * 4 + e];
-#else
         for (int e = tid; e < cn; e += kScoreNT) {
             const double* q = npts + (int64_t)(c0 + e) * 4;
             s_ptf[e] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
         }
-#endif
         __syncthreads();
         // one wave per model (2 or 4 models per wave pass over the chunk, reading each point
         // once, measured slower: 73.0 K vs 72.6 / 71.4 K frames/s, profiles/r02w_ab_score_dk.txt)
         for (int e = wid; e < T; e += kScoreNT / 64) {
-#if DVO_SCORE_BAIL && DVO_SCORE_F32 && DVO_SCORE_DEFER
             if (s_cnt[e] + s_pend[e] + (m - c0) <= bail) continue;  // wave-uniform: this wave's own model
-#endif
             int cnt = 0;
-#if DVO_SCORE_F32
             // undecided points (a sliver) are marked per lane and take the f64 test after the
             // chunk, only in the waves that have one
             SampsonF32 sf;
@@ -1693,7 +1642,6 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
                 cnt += __popcll(__ballot(d == 1));
                 umask |= (uint32_t)(d < 0) << k;
             }
-#if DVO_SCORE_DEFER
             if (m <= 0x10000 && __ballot(umask != 0)) {  // list the chunk's undecided points for the block's f64 pass
 #pragma unroll
                 for (int k = 0; k < kScoreChunk / 64; ++k) {
@@ -1715,8 +1663,6 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
                     }
                 }
             }
-#endif
-#ifndef DVO_EXP_SCORE_NO_F64  // timing experiment only: undecided points counted as outliers
             if (__ballot(umask != 0)) {
                 double Ed[9];
 #pragma unroll
@@ -1731,21 +1677,10 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
                     cnt += __popcll(__ballot(in));
                 }
             }
-#endif
-#else
-            double Ed[9];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) Ed[k] = s_E[e * 9 + k];
-            for (int j = lane; j < cn; j += 64) {
-                const double* pt = s_pts + j * 4;
-                cnt += __popcll(__ballot(sampson_inlier(Ed, pt[0], pt[1], pt[2], pt[3], t, fast_ok)));
-            }
-#endif
             if (lane == 0) s_cnt[e] += cnt;
         }
     }
     __syncthreads();
-#if DVO_SCORE_F32 && DVO_SCORE_DEFER
     {  // the block's deferred f64 tests, all at once
         const int nu = min(s_nund, kScoreUnd);
         for (int u = tid; u < nu; u += kScoreNT) {
@@ -1760,7 +1695,6 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
         }
         __syncthreads();
     }
-#endif
     for (int e = tid; e < T; e += kScoreNT) {
         int h = 0;
         while (h + 1 < hn && s_pref[h + 1] <= e) ++h;

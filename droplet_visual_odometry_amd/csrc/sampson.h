@@ -48,7 +48,7 @@ DVO_HD inline bool sampson_inlier(const double* E, double x1, double y1, double 
 }
 
 // The same decision from single-precision estimates, for the batched score
-// (DVO_SCORE_F32): it settles all but a sliver of the model-point pairs, and the
+// (ransac_score_kernel): it settles all but a sliver of the model-point pairs, and the
 // rest (and every value outside the ranges below) take sampson_inlier.  Inputs
 // rounded to f32 (relative error u = 2^-24 each), products and sums as FMAs.
 // With A_i = |E_i0 x1| + |E_i1 y1| + |E_i2|, B_i the same for E^T x2, and

@@ -1,5 +1,5 @@
 """The RANSAC score's deferred f64 Sampson tests (geometry.hip
-ransac_score_kernel, DVO_SCORE_DEFER): points the single-precision bounds
+ransac_score_kernel): points the single-precision bounds
 leave undecided are listed per block in LDS and tested in f64 after the last
 chunk; a full list falls back to the inline test.  A camera whose focal
 length is tiny makes every normalised coordinate large (> 1e6: outside
