@@ -1898,10 +1898,13 @@ StreamParams frame_group(const StreamParams& P, int f0, int n) {
 // (the group's pyramid is still in the caches when Harris and describe
 // re-read it).  Two-stream bench, whole batch 87.6-88.2 K; groups of 64 -8 %, 128 -2 %, 256
 // +0.8 to +1.5 %, 512 / 1024 +-0 (profiles/r04o_ab_describe_sincos_groups.txt, r04p_ab*.txt,
-// r04q_ab_orb_groups.txt); one stream alone is slower (small launches), two overlap better.  Stage
-// events: one table of 2 x 5 per group (orb_groups), summed per stage.
+// r04q_ab_orb_groups.txt); one stream alone is slower (small launches), two overlap better.  Re-swept
+// at batch 3072 on the round-4 final kernels: 256 90.8 K, 384 91.7 K, 512 91.7 K, 768 92.0 K, none
+// 90.6 K at C3; 137.1 / 139.0 / 140.4 / 141.1 / 139.7 K at C2 (profiles/r05b_ab_c3_orb_groups.txt,
+// r05b_ab_c2_orb_groups.txt).  Stage events: one table of 2 x 5 per group (orb_groups), summed per
+// stage.
 #ifndef DVO_ORB_GROUP
-#define DVO_ORB_GROUP 256
+#define DVO_ORB_GROUP 768
 #endif
 int orb_groups(int nframes) {
     const int grp = DVO_ORB_GROUP;

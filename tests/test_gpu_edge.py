@@ -195,20 +195,21 @@ def test_detect_noise_frame_long_lists(gpu_ctx, oracle_mod):
 
 
 def test_large_batch_equals_small_batches(gpu_ctx):
-    """A 300-frame batch (detection in two frame groups of 150, csrc/orb.hip launch_orb,
-    DVO_ORB_GROUP 256) gives every frame the features and every pair the record that 2-frame
-    batches of the same frames give, across the group boundary too (pair 149)."""
+    """An 800-frame batch (detection in two frame groups of 400, csrc/orb.hip launch_orb,
+    DVO_ORB_GROUP 768) gives every frame the features and every pair the record that 2-frame
+    batches of the same frames give, across the group boundary too (pair 399)."""
     import torch
     from droplet_visual_odometry_amd.stream import FrameStream
-    W, H, N, F = 320, 240, 300, 300
-    frames, K = synth_frames(W, H, range(F))
+    W, H, N, F = 320, 240, 300, 800
+    frames, K = synth_frames(W, H, range(F // 2))
+    frames = np.concatenate([frames, frames])  # pair 399 closes the loop back to frame 0
     big = FrameStream(W, H, K, nfeatures=N, max_frames=F, ctx=gpu_ctx)
     dev = torch.from_numpy(np.ascontiguousarray(frames)).cuda()
     rec = big.process(dev)
     big.sync()
     recs = FrameStream.records_numpy(rec, F - 1)
     small = FrameStream(W, H, K, nfeatures=N, max_frames=2, ctx=gpu_ctx)
-    for i in (0, 62, 148, 149, 150, 151, 255, 256, 298):
+    for i in (0, 62, 398, 399, 400, 401, 767, 768, 798):
         r2 = small.process(dev[i:i + 2])
         small.sync()
         for k in (0, 1):
