@@ -783,8 +783,8 @@ def hbm_roofline(stage, ms, W, H, N, B, m_avg):
             "stage": stage, "kernel": ", ".join(pmc["kernels"]) if pmc else " / ".join(STAGE_KERNELS[stage]),
             "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms_per_launch": round(ms, 4),
             "launch_note": "a launch = one batch (B + 1 frames or B pairs); detection stages run in frame groups of "
-                           "<= 256 (csrc/orb.hip DVO_ORB_GROUP), so rocprofv3's per-dispatch average for these "
-                           "kernels is this time divided by ceil((B + 1) / 256) dispatches"}
+                           "<= 768 (csrc/orb.hip DVO_ORB_GROUP), so rocprofv3's per-dispatch average for these "
+                           "kernels is this time divided by ceil((B + 1) / 768) dispatches"}
 
 
 def roofline_of(per_call, value, W, H, N, B, m_avg):
