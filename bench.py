@@ -97,7 +97,117 @@ def parse():
                          "chain over N x B gathered records on torch's stream beside the library streams (0 = skip)")
     ap.add_argument("--pose-check-32", type=int, default=24,
                     help="pairs of the OpenCV 3.2-semantics pose check against the oracle (0 = skip)")
+    ap.add_argument("--runs", type=int, default=5,
+                    help="timed runs of exactly --steps steps each; value = the median run (BASELINE.md §3: "
+                         "median of 5 runs), every run's rate reported under `runs`")
+    ap.add_argument("--pose-check-per-rank", type=int, default=6,
+                    help="N > 1: pairs at the start of every rank's run of the gathered window checked against "
+                         "the oracle (0 = skip)")
+    ap.add_argument("--spawn-check", action="store_true", help=argparse.SUPPRESS)  # tests/test_bench_launch.py
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) run directly, without torch.distributed.run: one
+    worker process per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
+    127.0.0.1), each re-running this script with the same arguments; only rank
+    0 prints the JSON line.  The parent starts them before anything touches the
+    GPU (torch.cuda.device_count() does not initialise a device on this image)
+    and never replaces itself: it waits, stops the other ranks when one fails
+    and exits with the first failure's status.  With RCCL (the default) N must
+    not exceed the node's GPUs; DVO_BENCH_BACKEND=gloo rehearses more ranks
+    than GPUs (ranks share devices, records gathered through host memory).
+    Under a launcher (WORLD_SIZE set) this is skipped."""
+    import subprocess
+    n = args.gpus
+    backend = os.environ.get("DVO_BENCH_BACKEND", "nccl")
+    if backend != "gloo" and not args.spawn_check:
+        import torch
+        have = torch.cuda.device_count()
+        if n > have:
+            print(f"bench.py: --gpus {n} needs {n} GPUs for RCCL, this node has {have} "
+                  f"(DVO_BENCH_BACKEND=gloo rehearses more ranks than GPUs)", file=sys.stderr, flush=True)
+            return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in sorted(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def spawn_check():
+    """The launcher rehearsal without a GPU (tests/test_bench_launch.py): every
+    rank joins the gloo group; rank 0 prints what each rank saw."""
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ["LOCAL_RANK"]), "pid": os.getpid(),
+                                  "world": dist.get_world_size()})
+    if rank == 0:
+        print(json.dumps({"spawn_check": seen}), flush=True)
+    dist.destroy_process_group()
+
+
+def timed_runs(args, step, sync_all, first, dist=None, device=None):
+    """args.runs timed runs of exactly args.steps steps each, every run
+    bracketed by a barrier (N > 1) and a device sync on both sides, its time
+    the max over ranks.  Returns the per-run seconds."""
+    import torch
+    out = []
+    i = first
+    for _ in range(max(1, args.runs)):
+        sync_all()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(i)
+            i += 1
+        sync_all()
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out.append(dt)
+    return out
+
+
+def runs_summary(per_run_s, units_per_run):
+    rates = [units_per_run / s for s in per_run_s]
+    med = float(np.median(rates))
+    return med, {"n": len(rates), "frames_per_s": [round(r, 1) for r in rates], "median": round(med, 2),
+                 "min": round(min(rates), 1), "max": round(max(rates), 1),
+                 "spread_frac": round((max(rates) - min(rates)) / med, 4),
+                 "note": "value = the median run; each run times exactly `steps` steps (BASELINE.md §3)"}
 
 
 def stage_bytes(w, h, nfeatures, n_matches):
@@ -121,6 +231,10 @@ def stage_bytes(w, h, nfeatures, n_matches):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.spawn_check:
+        return spawn_check()
     import torch
     import torch.distributed as dist
 
@@ -196,16 +310,16 @@ def main():
         for f in fss:
             f.set_profiling(True)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    sync_all()
-    elapsed = time.perf_counter() - t0
+    t_origin = time.perf_counter()
+    per_run = timed_runs(args, step, sync_all, args.warmup)
+    n_run = len(per_run)
     for i, t_a, t_b, t_c in host_log:
-        print(f"host step {i}: process enqueued at {1e3 * (t_a - t0):8.2f} ms, took {1e3 * (t_b - t_a):6.2f} ms; "
+        print(f"host step {i}: process enqueued at {1e3 * (t_a - t_origin):8.2f} ms, took {1e3 * (t_b - t_a):6.2f} ms; "
               f"pose_tail {1e3 * (t_c - t_b):6.2f} ms", file=sys.stderr)
+    value, runs = runs_summary(per_run, B * args.steps)
+    elapsed = B * args.steps / value  # the median run's time
 
-    recs = FrameStream.records_numpy(recs_t[(args.warmup + args.steps - 1) % S], B)
+    recs = FrameStream.records_numpy(recs_t[(args.warmup + n_run * args.steps - 1) % S], B)
     stage_ms, calls = {}, 0
     if not args.no_profile:
         for f in fss:
@@ -213,7 +327,6 @@ def main():
             calls += c
             for kk, v in sm.items():
                 stage_ms[kk] = stage_ms.get(kk, 0.0) + v
-    value = B * args.steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
     m_avg = float(np.mean(recs["n_matches"])) if len(recs) else N / 2
@@ -223,7 +336,7 @@ def main():
         per_call = {k: v / calls for k, v in stage_ms.items()}
         roofline = roofline_of(per_call, value, W, H, N, B, m_avg)
     # the other schedules of the same workload, on the GPU (never `value`)
-    i_last = args.warmup + args.steps - 1
+    i_last = args.warmup + n_run * args.steps - 1
     legs = {}
     def leg(name, fn, *a):
         # a leg that fails (e.g. out of device memory at an unusual batch) is reported, never the whole line
@@ -308,6 +421,7 @@ def main():
         "cpu_baseline": cpu,
         "pose_check": pose_check,
         "pose_check_opencv32": pose_check_32,
+        "runs": runs,
         "dropin": dropin,
         "legs": legs,
     }
@@ -609,21 +723,38 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
     for i in range(args.warmup):
         step(i)
     sync_all()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        recs = step(args.warmup + i)
+    if not args.no_profile:
+        for f in run.fss:
+            f.set_profiling(True)
+    per_run = timed_runs(args, step, sync_all, args.warmup, dist=dist,
+                         device=torch.device("cpu") if run.host_gather else dev)
+    value, runs = runs_summary(per_run, WP * args.steps)
+    elapsed = WP * args.steps / value
+    stage_ms, calls = {}, 0
+    if not args.no_profile:
+        for f in run.fss:
+            sm, c = f.stage_times()
+            calls += c
+            for kk, v in sm.items():
+                stage_ms[kk] = stage_ms.get(kk, 0.0) + v
+            f.set_profiling(False)
+    # window 0 once more, every rank: its gathered records are what rank 0 checks against the oracle
+    recs = run.step(pools[0], corners[0][:-1], corners[0][1:], wait_torch=False)[0]
     sync_all()
-    dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if run.host_gather else dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    recs = recs.cpu().numpy().view(PAIR_RECORD_DTYPE)
-    value = WP * args.steps / elapsed
+    recs = recs.cpu().numpy().view(PAIR_RECORD_DTYPE).copy()
     if rank == 0:
         m_avg = float(np.mean(recs["n_matches"]))
+        roofline = None
+        if stage_ms and calls:
+            per_call = {k: v / calls for k, v in stage_ms.items()}
+            roofline = roofline_of(per_call, value / world, W, H, N, run.n_local, m_avg)
+            roofline["rank"] = 0
+            roofline["note_sharded"] = ("rank 0's HIP-event stages over its own runs (n_local + 1 frames, n_local "
+                                        "pairs per launch); path_frac per GPU")
+        cpu = pose_check = None
+        if args.cpu_seconds > 0:
+            cpu, ref = cpu_baseline(pools[0], scene.K, N, args.max_iters, args.cpu_seconds)
+            pose_check = sharded_pose_check(args, scene, recs, ref, world, WP)
         out = {
             "metric": ("frames/sec (detect+match+pose) at 1280\u00d7720, 2000 feats; ATE vs reference"
                        if (W, H, N) == (1280, 720, 2000)
@@ -645,14 +776,64 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
                        "parallelism": f"one stream pair-sharded x{world} + "
                                       + ("gloo all_gather (rehearsal)" if run.host_gather else "RCCL all_gather")
                                       + " of records and marker corners, rank-0 device pose tail and chain",
-                       "streams_in_flight": S,
+                       "streams_in_flight": S, "rccl_world": dist.get_world_size(),
+                       "backend": "gloo" if run.host_gather else "nccl (RCCL)",
+                       "pairs_per_rank": run.n_local, "window_pairs": WP,
                        "pairs_ok": f"{int(np.sum(recs['status'] == 0))}/{len(recs)}", "mean_matches": round(m_avg, 1),
-                       "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1)},
-            "roofline": None,
-            "cpu_baseline": None,
+                       "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1),
+                       "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "pose_check": pose_check,
+            "runs": runs,
         }
+        if cpu is not None:
+            out["speedup_vs_cpu_same_mode"] = {"streaming": round(value / max(cpu["value"], 1e-9), 1),
+                                               "cpu_threads": cpu["cores"]}
         print(json.dumps(out), flush=True)
+    dist.barrier()  # the other ranks wait for rank 0's checks before the group goes away
+    run.close()
     dist.destroy_process_group()
+
+
+def sharded_pose_check(args, scene, recs, ref, world, WP):
+    """R, t of the gathered window-0 records against the oracle: rank 0's
+    pairs from cpu_baseline's sequential sample (`ref`), and the first
+    --pose-check-per-rank pairs of every other rank's run, each run's oracle
+    pass starting, as that rank does, from a fresh detect of its first frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from droplet_visual_odometry_amd import dist as ddist
+    from droplet_visual_odometry_amd.synth import MARKER_LEN  # noqa: F401
+    K, N = scene.K, args.nfeatures
+    host = lambda g: scene.render(g).cpu().numpy()  # noqa: E731
+    checked = []  # (global pair, R_ref, t_ref)
+    for i, (R, t) in enumerate(ref[:max(1, args.pose_check_per_rank)]):
+        checked.append((i, R, t))
+    for r in range(1, world):
+        p0, p1, _, _ = ddist.shard_window(WP, world, r, 0)
+        n = min(args.pose_check_per_rank, p1 - p0)
+        if n <= 0:
+            continue
+        kp = oracle.detect_and_compute(host(p0), N)
+        for p in range(p0, p0 + n):
+            o = oracle.pair_pose(host(p), host(p + 1), K, N, max_iters=args.max_iters, kp_prev=kp)
+            kp = (o["kp_cur"], o["desc_cur"])
+            checked.append((p, o["R"], o["t_unit"]))
+    ident = 0
+    err_r = err_t = 0.0
+    for p, R_ref, t_ref in checked:
+        if R_ref is None:
+            ident += int(recs["status"][p] != 0)
+            continue
+        Rg, tg = recs["R"][p].reshape(3, 3), recs["t"][p]
+        ident += int(np.array_equal(Rg, R_ref) and np.array_equal(tg, np.asarray(t_ref).ravel()))
+        err_r = max(err_r, float(np.max(np.abs(Rg - R_ref))))
+        err_t = max(err_t, float(np.max(np.abs(tg - np.asarray(t_ref).ravel()))))
+    return {"pairs": len(checked), "bit_identical": ident, "max_abs_R_err": err_r, "max_abs_t_err": err_t,
+            "ranks_checked": world, "pairs_checked": sorted({p for p, _, _ in checked}),
+            "reference": "oracle/ C++ restatement, same frames, streaming with feature reuse from each rank's first "
+                         "frame; records from the all-gathered window 0"}
 
 
 def chained_ate(fs, pool, corners, K, ref, B):

@@ -78,6 +78,7 @@ struct dvo_stream {
     int32_t* fc_n = nullptr;  // nkp, status
     dvo_pair_record* pair_rec = nullptr;
     bool fc_valid = false;
+    bool last_reuse = false;  // the last call was dvo_stream_pair(reuse_prev): pyramid slot 0 holds frame 1
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
     std::vector<std::vector<hipEvent_t>> ev_pending;
@@ -538,6 +539,7 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
     HIP_TRY(launch_orb(P, s->hs, ev, ev && groups ? ev + 2 * DVO_NSTAGES : nullptr));
     s->last_nframes = n;
+    s->last_reuse = false;
     s->last_frames = d_frames;
     s->last_fstride = fstride;
     s->last_pitch = pitch;
@@ -789,12 +791,15 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     if (s->cfg.max_frames < 2) return fail(ctx, DVO_EINVAL, "dvo_stream_pair needs max_frames >= 2");
     if (!cur_img || !rec_out || stride < w || (!reuse_prev && !prev_img)) return fail(ctx, DVO_EINVAL, "bad image buffer");
     if (reuse_prev && !s->fc_valid) return fail(ctx, DVO_EINVAL, "reuse_prev needs a preceding dvo_stream_pair");
+    // the feature cache is valid only after a call that succeeds (a failing call may have left
+    // its frame half-way through the rotation)
+    s->fc_valid = false;
     HIP_TRY(hipSetDevice(ctx->device));
     const size_t kc = (size_t)s->plan.kp_cap;
-    if (!s->fc_kps) {
+    if (!s->pair_rec) {  // each buffer once: a partial failure leaves the rest to the next call
         int rc;
-        if ((rc = dalloc(s, &s->fc_kps, kc)) || (rc = dalloc(s, &s->fc_desc, kc * 32)) ||
-            (rc = dalloc(s, &s->fc_n, 2)) || (rc = dalloc(s, &s->pair_rec, 1)))
+        if ((!s->fc_kps && (rc = dalloc(s, &s->fc_kps, kc))) || (!s->fc_desc && (rc = dalloc(s, &s->fc_desc, kc * 32))) ||
+            (!s->fc_n && (rc = dalloc(s, &s->fc_n, 2))) || (rc = dalloc(s, &s->pair_rec, 1)))
             return rc;
     }
     Staging st;
@@ -815,6 +820,9 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     };
     const int64_t fst = (int64_t)pw * h;
     const Buffers& b = s->buf;
+    // after the first upload, an error drains the stream before returning: its DMAs read the
+    // context's pinned staging area, which the next staging user rewrites (or frees to grow it)
+    auto body = [&]() -> int {
     // the feature arrays of frame 0, frame 1 and the cache (the last current frame's), in 4-byte words
     FeatSlots fsl{};
     auto slot = [&](int k, void* kps, void* desc, int32_t* n, int32_t* stt) {
@@ -851,7 +859,14 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     HIP_TRY(st.get(s->pair_rec, sizeof(dvo_pair_record), &hr));
     HIP_TRY(hipStreamSynchronize(s->hs));
     std::memcpy(rec_out, hr, sizeof(dvo_pair_record));
+    return DVO_OK;
+    };
+    if ((rc = body())) {
+        (void)hipStreamSynchronize(s->hs);
+        return rc;
+    }
     s->fc_valid = true;
+    s->last_reuse = reuse_prev != 0;
     s->last_nframes = 2;
     s->last_pairs = 1;
     s->last_has_pairs = true;
@@ -918,13 +933,20 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
     dvo_ctx* ctx = s->ctx;
     if (frame < 0 || frame >= s->last_nframes || level < 0 || level >= s->plan.nlevels)
         return fail(ctx, DVO_EINVAL, "frame/level out of range");
+    int nfr = s->last_nframes;
+    if (s->last_reuse) {  // dvo_stream_pair(reuse_prev) detected frame 1 alone, into pyramid slot 0
+        if (frame == 0)
+            return fail(ctx, DVO_EINVAL, "after dvo_stream_pair(reuse_prev) only frame 1's pyramid is kept");
+        frame = 0;
+        nfr = 1;
+    }
     const LevelGeom& G = s->plan.L[level];
     if (cap < G.w * G.h) return fail(ctx, DVO_ECAP, "capacity too small");
     HIP_TRY(hipStreamSynchronize(s->hs));
     if (blurred) {
         // the detection path blurs only the descriptor windows (describe_kernel): the whole blurred
         // pyramid is recomputed here from the last call's frames, which must still be alive
-        HIP_TRY(launch_blur(params_of(s, s->last_frames, s->last_nframes, s->last_fstride, s->last_pitch), s->hs));
+        HIP_TRY(launch_blur(params_of(s, s->last_frames, nfr, s->last_fstride, s->last_pitch), s->hs));
         HIP_TRY(hipStreamSynchronize(s->hs));
     }
     if (blurred) {

@@ -240,7 +240,11 @@ int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs
  * equal the operator-by-operator path's (the per-call RANSAC schedule: one
  * round, n_hypotheses as dvo_find_essential_mat).  reuse_prev = 1: the
  * previous frame is the last call's current frame, whose features the stream
- * kept on the device (prev_img may be NULL), so only cur_img is detected.
+ * kept on the device (prev_img may be NULL), so only cur_img is detected;
+ * that cache is valid only after a call that returned DVO_OK (a failing call
+ * invalidates it, and reuse_prev is then refused).  After a reuse_prev call,
+ * dvo_stream_get_pyramid has frame 1 only (the previous frame's pyramid is not
+ * kept); get_features has both frames.
  * Images: w x h mono8, rows `stride` bytes apart.  Needs max_frames >= 2. */
 int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_img, int stride, int reuse_prev,
                     dvo_pair_record* rec_out);

@@ -2,7 +2,7 @@
 `-D` macro sets, for A/B stage timing on the GPU box via DVO_LIB_PATH.
 usage: python tools/build_variants.py TAG=MACRO[,MACRO...] ...
 (a spec containing '|' is split on '|' instead, for macro values with commas:
- r3=DVO_RANSAC_BOUNDS=64,256,1073741824)"""
+ r3='DVO_RANSAC_BOUNDS=64,256,1073741824|' -- the '|' is required for those)"""
 import os
 import sys
 
@@ -13,5 +13,5 @@ for spec in sys.argv[1:]:
     tag, _, macros = spec.partition("=")
     out = os.path.join(LIBDIR, "exp", f"libdvo_{tag}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    sep = "|" if "|" in macros or macros.count("=") == 1 and macros.count(",") > 0 else ","
+    sep = "|" if "|" in macros else ","
     print(build(force=True, out=out, defines=[m for m in macros.split(sep) if m]))
