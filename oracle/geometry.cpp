@@ -252,7 +252,9 @@ int solve_cubic(const double* c, double* x) {
 // mathfuncs.cpp solvePoly (Durand-Kerner, Gauss-Seidel order).  coeffs[0..n0]
 // ascending.  Returns the working degree n; roots beyond it are not reported
 // (OpenCV leaves them as uninitialised buffer contents).
-int solve_poly(const double* rc, int n0, int max_iters, Cx* roots) {
+// trace (analysis only, tools/dk_cycle_stats.py): a 64-bit hash of the roots' bits after each
+// sweep, trace[max_iters] = the sweeps run (the maxDiff <= 0 exit or max_iters).
+int solve_poly(const double* rc, int n0, int max_iters, Cx* roots, uint64_t* trace = nullptr) {
     std::vector<Cx> coeffs(n0 + 1);
     for (int i = 0; i <= n0; i++) coeffs[i] = Cx{rc[i], 0};
     int n = n0;
@@ -307,6 +309,18 @@ int solve_poly(const double* rc, int n0, int max_iters, Cx* roots) {
             }
             roots[i] = csub(p, num);
             maxDiff = std::max(maxDiff, cabs(num));
+        }
+        if (trace) {
+            uint64_t hsh = 1469598103934665603ull;
+            for (int i = 0; i < n; i++) {
+                uint64_t a, b;
+                std::memcpy(&a, &roots[i].re, 8);
+                std::memcpy(&b, &roots[i].im, 8);
+                hsh = (hsh ^ a) * 1099511628211ull;
+                hsh = (hsh ^ b) * 1099511628211ull;
+            }
+            trace[iter] = hsh;
+            trace[max_iters] = (uint64_t)(iter + 1);
         }
         if (maxDiff <= 0) break;
     }
@@ -411,6 +425,8 @@ void poly_mul(const double* a, int na, const double* b, int nb, double* r) {  //
 }
 
 // five-point.cpp EMEstimatorCallback::runKernel on 5 normalised correspondences.
+thread_local double t_last_poly[11];  // the last five_point's degree-10 polynomial (analysis hook)
+
 int five_point(const double* q1, const double* q2, double* models) {
     // Q (5x9), then SVD::compute(Q, W, U, Vt, MODIFY_A | FULL_UV): m<n so the
     // 5 rows are orthogonalised as At (m=9, n=5) and completed to 9 rows;
@@ -485,6 +501,7 @@ int five_point(const double* q1, const double* q2, double* models) {
     poly_mul(pc[0], 5, m3, 7, t3);
     for (int k = 0; k < 11; ++k) c[k] = (t1[k] - t2[k]) + t3[k];
 
+    std::memcpy(t_last_poly, c, sizeof(t_last_poly));
     Cx roots[10];
     int nr = solve_poly(c, 10, 300, roots);
     int count = 0;
@@ -620,6 +637,16 @@ int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_i
 int ora_five_point(const double* p1, const double* p2, double* models, int* n) {
     *n = five_point(p1, p2, models);
     return 0;
+}
+
+int ora_last_five_point_poly(double* c) {
+    std::memcpy(c, t_last_poly, sizeof(t_last_poly));
+    return 0;
+}
+
+int ora_solve_poly_trace(const double* coeffs, int n, int max_iters, uint64_t* trace) {
+    std::vector<Cx> r(n);
+    return solve_poly(coeffs, n, max_iters, r.data(), trace);
 }
 
 int ora_find_essential(const double* p1, const double* p2, int m, const double* K, double prob, double threshold,

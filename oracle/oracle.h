@@ -94,6 +94,10 @@ int ora_five_point(const double* p1, const double* p2, double* models, int* n);
 // Helpers exposed for unit KATs.
 int ora_jacobi_svd(double* At, int m, int n, int n1, double* W, double* Vt);
 int ora_solve_poly(const double* coeffs, int n, int max_iters, double* roots /*2n*/);
+// Analysis hooks (tools/dk_cycle_stats.py): the polynomial of this thread's last
+// ora_five_point, and solvePoly's per-sweep root-state hashes (trace[max_iters] = sweeps run).
+int ora_last_five_point_poly(double* c /*11*/);
+int ora_solve_poly_trace(const double* coeffs, int n, int max_iters, uint64_t* trace /*max_iters + 1*/);
 int ora_ransac_update_num_iters(double p, double ep, int model_points, int max_iters);
 // RANSAC pieces pinned separately: getSubset's draws (n x 5) and the sequential
 // best / niters bookkeeping over per-hypothesis counts (cnt: n x 10);

@@ -23,6 +23,8 @@ A = None
 
 
 def _detect(i):
+    import torch
+    torch.set_num_threads(1)
     from droplet_visual_odometry_amd.synth import SceneStream
     st = SceneStream(A.width, A.height)
     img = st.render(i).numpy()
@@ -62,6 +64,10 @@ def _counts(job):
             err = (r * r / (ex0 * ex0 + ex1 * ex1 + et0 * et0 + et1 * et1)).astype(np.float32)
             cnt[h, k] = int(np.sum(err <= tf))
     return m, cnt
+
+
+def _init():
+    os.environ["OMP_NUM_THREADS"] = "1"
 
 
 def update(ep, niters):
@@ -115,7 +121,7 @@ def main():
         z = np.load(A.cache)
         ms, cnts = z["m"], z["cnt"]
     else:
-        with Pool(8) as pool:
+        with Pool(8, initializer=_init) as pool:
             det = pool.map(_detect, range(A.pairs + 1))
             K = det[0][1]
             jobs = [(det[i][0][0], det[i][0][1], det[i + 1][0][0], det[i + 1][0][1], K, A.max_iters)
