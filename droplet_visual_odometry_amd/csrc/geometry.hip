@@ -2278,15 +2278,7 @@ __device__ __forceinline__ double quad_bcast(double v) {  // lane 4 q + K of the
     const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), ctl, 0xF, 0xF, false);
     return __builtin_bit_cast(double, ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
-// The chain is one wave's dependency chain; beside a batch's kernels on the other streams
-// (rank 0 of a sharded run, bench.py legs.rank0_tail_world8) it shares its SIMD with their
-// waves, so it raises its wave priority: the SIMD's arbiter then issues its next instruction
-// first whenever it is ready (DVO_CHAIN_PRIO 0 = off).
-#ifndef DVO_CHAIN_PRIO
-#define DVO_CHAIN_PRIO 3
-#endif
 __global__ __launch_bounds__(64) void pose_chain_kernel(TailArgs a) {
-    if constexpr (DVO_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(DVO_CHAIN_PRIO);
     constexpr int kChunk = 64, kPer = kChunk * 16 / 64;  // T_rel doubles per lane and chunk
     __shared__ double tr[kChunk * 16];
     __shared__ double ob[kChunk * 16];  // the chunk's T_abs, stored to global memory coalesced
