@@ -275,13 +275,13 @@ def main():
            for _ in range(S)]
     for f in fss[1:]:
         f.share_pose(fss[0])  # one pose stream across the alternating batches
-    recs_t = [f.new_records(B) for f in fss]
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     corners = torch.tensor(np.stack([scene.marker_corners(i) for i in range(pool_n)]), dtype=torch.float64,
                            device=dev)
     T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     fss[0].reset_pose()
+    pipe = Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
     torch.cuda.synchronize()
     n_windows = max(1, (pool_n - 1) // B)
 
@@ -289,21 +289,14 @@ def main():
 
     def step(i):
         s = (i % n_windows) * B
-        k = i % S
-        fs = fss[k]
         t_a = time.perf_counter()
-        fs.process(pool[s:s + B + 1], recs_t[k], wait_torch=False)
-        t_b = time.perf_counter()
-        fs.pose_tail(corners[s:s + B], corners[s + 1:s + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
+        pipe.step(i % S, pool[s:s + B + 1], s)
         if args.host_trace:
-            host_log.append((i, t_a, t_b, time.perf_counter()))
+            host_log.append((i, t_a, time.perf_counter(), time.perf_counter()))
 
-    def sync_all():
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
-
-    for i in range(args.warmup):
+    sync_all = pipe.sync
+    prime = max(args.warmup, pipe.prime_steps)  # the pipeline is full: every timed step retires one batch
+    for i in range(prime):
         step(i)
     sync_all()
     if not args.no_profile:
@@ -311,15 +304,13 @@ def main():
             f.set_profiling(True)
     torch.cuda.synchronize()
     t_origin = time.perf_counter()
-    per_run = timed_runs(args, step, sync_all, args.warmup)
+    per_run = timed_runs(args, step, sync_all, prime)
     n_run = len(per_run)
     for i, t_a, t_b, t_c in host_log:
-        print(f"host step {i}: process enqueued at {1e3 * (t_a - t_origin):8.2f} ms, took {1e3 * (t_b - t_a):6.2f} ms; "
-              f"pose_tail {1e3 * (t_c - t_b):6.2f} ms", file=sys.stderr)
+        print(f"host step {i}: submit enqueued at {1e3 * (t_a - t_origin):8.2f} ms, took {1e3 * (t_b - t_a):6.2f} ms",
+              file=sys.stderr)
     value, runs = runs_summary(per_run, B * args.steps)
     elapsed = B * args.steps / value  # the median run's time
-
-    recs = FrameStream.records_numpy(recs_t[(args.warmup + n_run * args.steps - 1) % S], B)
     stage_ms, calls = {}, 0
     if not args.no_profile:
         for f in fss:
@@ -327,6 +318,13 @@ def main():
             calls += c
             for kk, v in sm.items():
                 stage_ms[kk] = stage_ms.get(kk, 0.0) + v
+            f.set_profiling(False)
+    t_d = time.perf_counter()
+    pipe.drain()
+    sync_all()
+    drain_ms = 1e3 * (time.perf_counter() - t_d)
+    recs = FrameStream.records_numpy(*pipe.last)
+    rec_ref = pipe.last
     ms_per_step = 1000.0 * elapsed / args.steps
 
     m_avg = float(np.mean(recs["n_matches"])) if len(recs) else N / 2
@@ -336,7 +334,6 @@ def main():
         per_call = {k: v / calls for k, v in stage_ms.items()}
         roofline = roofline_of(per_call, value, W, H, N, B, m_avg)
     # the other schedules of the same workload, on the GPU (never `value`)
-    i_last = args.warmup + n_run * args.steps - 1
     legs = {}
     def leg(name, fn, *a):
         # a leg that fails (e.g. out of device memory at an unusual batch) is reported, never the whole line
@@ -349,15 +346,15 @@ def main():
 
     if not args.no_ref_equivalent:
         leg("reference_equivalent", ref_equivalent_leg, args, pool, corners, scene.K, ctx, value, recs,
-            (i_last % n_windows) * B)
+            pipe.last_s0)
     if not args.no_host_fed:
         for f in fss:
             f.set_profiling(False)
-        leg("host_fed", host_fed_leg, args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, value)
+        leg("host_fed", host_fed_leg, args, pool, pipe, n_windows, value)
     if args.tail_world > 1:
         for f in fss:
             f.set_profiling(False)
-        leg(f"rank0_tail_world{args.tail_world}", rank0_tail_leg, args, pool, fss, recs_t, corners, n_windows,
+        leg(f"rank0_tail_world{args.tail_world}", rank0_tail_leg, args, pool, pipe, corners, n_windows,
             scene.K, ctx)
 
     cpu = None
@@ -370,10 +367,13 @@ def main():
             re = legs["reference_equivalent"]
             re["cpu_value"] = cpu["reference_equivalent"]["value"]
             re["speedup_vs_cpu_same_mode"] = round(re["value"] / max(re["cpu_value"], 1e-9), 1)
-        # the same pairs on the GPU (window 0), compared with the oracle's R, t
-        fss[0].process(pool[0:B + 1], recs_t[0], wait_torch=False)
+        # the same pairs on the GPU (window 0, through the pipelined submit), compared with the oracle's R, t
+        rec0 = fss[0].new_records(B)
+        torch.cuda.synchronize()
+        fss[0].submit(pool[0:B + 1], rec0, wait_torch=False)
+        fss[0].drain()
         fss[0].sync()
-        g = FrameStream.records_numpy(recs_t[0], B)
+        g = FrameStream.records_numpy(rec0, B)
         n = min(len(ref), B)
         ident = 0
         err_r = err_t = 0.0
@@ -416,7 +416,14 @@ def main():
                    "streams_in_flight": S,
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0,
-                   "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0},
+                   "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0,
+                   "ransac_pipeline": {"depth": pipe.D, "prime_steps": max(args.warmup, pipe.prime_steps),
+                                       "drain_ms": round(drain_ms, 3),
+                                       "note": "RANSAC rounds of the last `depth` batches of a stream run as one "
+                                               "merged round per submit (include/dvo.h dvo_stream_submit); after "
+                                               "prime_steps untimed submits every timed step retires one complete "
+                                               "batch (records + pose tail); records identical to one batch at a "
+                                               "time (tests/test_gpu_pipeline.py)"}},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "pose_check": pose_check,
@@ -434,18 +441,78 @@ def main():
     print(json.dumps(out), flush=True)
 
 
+class Pipeline:
+    """Batches in flight on S library streams (dvo_stream_submit, include/dvo.h): stream k takes
+    steps k, k + S, ...; each submit runs detection + matching of its batch and one merged RANSAC
+    round of the stream's last pipeline_depth() batches, and retires the oldest, whose pose tail
+    (marker scale, relative and absolute poses, v3:309-345, :367) then runs on the shared carry in
+    step order.  After prime_steps submits every step retires exactly one batch of B pairs.
+    Each stream keeps pipeline_depth() record buffers in a ring (a batch's records stay pending
+    until it retires)."""
+
+    def __init__(self, fss, B, corners, marker_len, T_rel, T_abs, paired=False, tail=True):
+        from droplet_visual_odometry_amd.stream import FrameStream
+        import collections
+        self.fss, self.B, self.corners, self.L = fss, B, corners, marker_len
+        self.T_rel, self.T_abs, self.paired, self.tail = T_rel, T_abs, paired, tail
+        self.D = FrameStream.pipeline_depth()
+        self.recs = [[f.new_records(B) for _ in range(self.D)] for f in fss]
+        self.fifo = [collections.deque() for _ in fss]  # (first frame, global submit number) per pending batch
+        self.nsub = [0] * len(fss)
+        self.gseq = 0
+        self.last = None      # (records, pairs) of the last retired batch
+        self.last_s0 = None   # its first frame in the pool
+        self.prime_steps = len(fss) * (self.D - 1)
+        self.on_retire = None  # optional hook(k, records, pairs, s0) instead of the pose tail
+
+    def step(self, k, frames, s0, wait_torch=False):
+        fs = self.fss[k]
+        rec = self.recs[k][self.nsub[k] % self.D]
+        self.nsub[k] += 1
+        self.fifo[k].append((s0, self.gseq))
+        self.gseq += 1
+        ret = (fs.submit_pairs if self.paired else fs.submit)(frames, rec, wait_torch=wait_torch)
+        for r, pairs in ret:
+            self._retired(k, r, pairs, self.fifo[k].popleft()[0])
+
+    def _retired(self, k, r, pairs, s0):
+        if self.on_retire is not None:
+            self.on_retire(k, r, pairs, s0)
+        elif self.tail:
+            c = self.corners
+            self.fss[k].pose_tail_batch(r, pairs, c[s0:s0 + pairs], c[s0 + 1:s0 + pairs + 1], self.L, self.T_rel[k],
+                                        self.T_abs[k])
+        self.last, self.last_s0 = (r, pairs), s0
+
+    def drain(self):
+        # every stream's remaining rounds, then the pose tails in submission order (one carry)
+        done = []
+        for k, fs in enumerate(self.fss):
+            for r, pairs in fs.drain():
+                s0, g = self.fifo[k].popleft()
+                done.append((g, k, r, pairs, s0))
+        for g, k, r, pairs, s0 in sorted(done, key=lambda t: t[0]):
+            self._retired(k, r, pairs, s0)
+
+    def sync(self):
+        import torch
+        for f in self.fss:
+            f.sync()
+        torch.cuda.synchronize()
+
+
 def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, stream_first_pair):
     """The reference's own schedule on the GPU: visual_odometry_calculations
     re-detects BOTH frames of every pair (visual_odometry_v3.py:387-392), so a
-    step of B pairs detects 2B frames (FrameStream.process_pairs /
-    dvo_stream_process_pairs: pair p = frames 2p, 2p+1), then matches, RANSAC,
-    recoverPose and the pose tail as the streaming step.  The paired frame
-    tensors are gathered from the same device pool before timing.  Its
-    records must equal the streaming schedule's byte for byte (detection is
-    a function of the frame), which is checked on the streaming run's last
-    window.  Steps carry min(batch, 1024) pairs (2 x that many frames per
-    stream, beside the streaming run's streams, which stay allocated: a
-    stream holds ~16 MB of worst-case candidate and RANSAC buffers per frame)."""
+    step of B pairs detects 2B frames (FrameStream.submit_pairs /
+    dvo_stream_submit_pairs: pair p = frames 2p, 2p+1), then matches, RANSAC,
+    recoverPose and the pose tail as the streaming step (pipelined the same
+    way).  The paired frame tensors are gathered from the same device pool
+    before timing.  Its records must equal the streaming schedule's byte for
+    byte (detection is a function of the frame), which is checked on the
+    streaming run's last batch.  Steps carry min(batch, 1024) pairs (2 x that
+    many frames per stream, beside the streaming run's streams, which stay
+    allocated)."""
     import torch
     from droplet_visual_odometry_amd.stream import FrameStream
     from droplet_visual_odometry_amd.synth import MARKER_LEN
@@ -458,65 +525,61 @@ def ref_equivalent_leg(args, pool, corners, K, ctx, stream_value, stream_recs, s
     fss = [FrameStream(W, H, K, nfeatures=N, max_frames=2 * B, max_iters=args.max_iters, ctx=ctx) for _ in range(S)]
     for f in fss[1:]:
         f.share_pose(fss[0])
-    recs = [f.new_records(B) for f in fss]
     T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     fss[0].reset_pose()
+    pipe = Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs, paired=True)
     torch.cuda.synchronize()
 
     def step(i):
-        w, k = i % n_windows, i % S
-        s0 = w * B
-        fss[k].process_pairs(pp[w], recs[k], wait_torch=False)
-        fss[k].pose_tail(corners[s0:s0 + B], corners[s0 + 1:s0 + B + 1], MARKER_LEN, T_rel[k], T_abs[k],
-                         wait_torch=False)
+        w = i % n_windows
+        pipe.step(i % S, pp[w], w * B)
 
-    def sync_all():
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
-
-    for i in range(args.warmup):
+    prime = max(args.warmup, pipe.prime_steps)
+    for i in range(prime):
         step(i)
-    sync_all()
+    pipe.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
-    sync_all()
+        step(prime + i)
+    pipe.sync()
     dt = time.perf_counter() - t0
-    # the streaming run's last window (its first B pairs) through the paired schedule: identical records
+    pipe.drain()
+    pipe.sync()
+    # the streaming run's last batch (its first B pairs) through the paired schedule: identical records
     chk = pool.index_select(0, torch.tensor([stream_first_pair + p + j for p in range(B) for j in (0, 1)],
                                             device=dev)).contiguous()
-    fss[0].process_pairs(chk, recs[0], wait_torch=True)  # chk is written on torch's stream
+    rec = fss[0].process_pairs(chk, wait_torch=True)  # chk is written on torch's stream
     fss[0].sync()
     # every field the pair path defines (`reserved` carries pose-tail state of whichever window ran last)
-    got = FrameStream.records_numpy(recs[0], B)
+    got = FrameStream.records_numpy(rec, B)
     differing = [k for k in got.dtype.names if not np.array_equal(got[k], stream_recs[:B][k])]
     same = not [k for k in differing if k not in ("reserved", "pad0")]
     for f in fss:
         f.close()
-    del pp, fss, recs
+    del pp, fss, pipe
     torch.cuda.empty_cache()
     value = B * args.steps / dt
     return {"value": round(value, 2), "unit": "frames/s", "ms_per_step": round(1e3 * dt / args.steps, 3),
             "frames_detected_per_step": 2 * B, "pairs_per_step": B, "vs_streaming": round(value / stream_value, 4),
             "records_identical_to_streaming": same, "record_fields_differing": differing,
             "schedule": "reference-equivalent: both frames of every pair detected (v3:387-392), 2B detections "
-                        "per B pairs, two batches in flight; value counts pairs (= new frames of the stream)"}
+                        "per B pairs, two batches in flight, RANSAC rounds pipelined as the streaming run; value "
+                        "counts pairs (= new frames of the stream)"}
 
 
-def host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, stream_value):
+def host_fed_leg(args, pool, pipe, n_windows, stream_value):
     """Frames arriving from host memory, as the ROS harness hands them over
     (trajectory_evaluation_dual_process.py:154-164): the pool is held in
     pinned host memory, each step's B + 1 frames are copied host-to-device
-    on a copy stream into a ring of device slots (one more slot than batches
-    in flight), and the library stream waits for the copy's event, so the
-    H2D copy of step i+1 overlaps the compute of step i.  The link rate is
+    on a copy stream into a ring of device slots, and the library stream waits
+    for the copy's event, so the H2D copies of the next steps overlap the
+    compute of this one.  A slot is free again once the submit that read it
+    has run its detection (the frames are read only there).  The link rate is
     the same copies timed alone.  Never `value`."""
     import torch
-    from droplet_visual_odometry_amd.synth import MARKER_LEN
-    B, S = args.batch, len(fss)
-    R = S + 1
+    B, S = args.batch, len(pipe.fss)
+    R = S + 2  # copies run up to two steps ahead of the compute
     hpool = torch.empty(pool.shape, dtype=pool.dtype, pin_memory=True)
     hpool.copy_(pool)
     slots = [torch.empty((B + 1,) + tuple(pool.shape[1:]), dtype=pool.dtype, device=pool.device) for _ in range(R)]
@@ -528,29 +591,26 @@ def host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, stre
         s0, k, r = (i % n_windows) * B, i % S, i % R
         with torch.cuda.stream(cs):
             if used[r] is not None:
-                cs.wait_event(used[r])  # the compute that last read this slot has finished
+                cs.wait_event(used[r])  # the detection that last read this slot has finished
             slots[r].copy_(hpool[s0:s0 + B + 1], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cs)
-        fs = fss[k]
+        fs = pipe.fss[k]
         fs.wait_event(ev)
-        fs.process(slots[r], recs_t[k], wait_torch=False)
-        fs.pose_tail(corners[s0:s0 + B], corners[s0 + 1:s0 + B + 1], MARKER_LEN, T_rel[k], T_abs[k], wait_torch=False)
+        pipe.step(k, slots[r], s0)
         used[r] = fs.record_event()
 
-    def sync_all():
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
-
-    for i in range(args.warmup):
+    prime = max(args.warmup, pipe.prime_steps)
+    for i in range(prime):
         step(i)
-    sync_all()
+    pipe.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
-    sync_all()
+        step(prime + i)
+    pipe.sync()
     dt = time.perf_counter() - t0
+    pipe.drain()
+    pipe.sync()
     # the link alone: the same copies back to back on the copy stream
     nb = slots[0].numel()
     reps = max(3, min(args.steps, 10))
@@ -570,27 +630,27 @@ def host_fed_leg(args, pool, fss, recs_t, corners, T_rel, T_abs, n_windows, stre
             "h2d_bytes_per_step": nb, "h2d_link_GBps": round(link, 2),
             "link_bound_frames_per_s": round(link * 1e9 / (nb / (B + 1)) * B / (B + 1), 1),
             "vs_device_resident": round(value / stream_value, 4),
-            "schedule": "pinned host frames, async H2D on a copy stream into a ring of S+1 device slots "
-                        "overlapped with compute; B+1 frames copied per B-pair step"}
+            "schedule": "pinned host frames, async H2D on a copy stream into a ring of S+2 device slots overlapped "
+                        "with compute; B+1 frames copied per B-pair step"}
 
 
-def rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows, K, ctx):
+def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
     """Rank 0's added load in a world-N run (bench.main_sharded, dist.ShardedStreamRunner), rehearsed on one
-    GPU: per step the library streams process B new pairs as every rank does, and torch's stream -- after
-    waiting for that step's records, as before the all-gather -- runs the pose tail and the serial absolute
-    chain over a whole world-N window, N x B records (stream.PoseTail / dvo_pose_tail_records), as rank 0
-    does after the collective.  The gathered window is this rank's B records and corners tiled N times (the
-    tail's cost does not depend on their values).  Reported: ms per step with and without the rank-0 tail
-    and the difference, against north_star's near-linear scaling (trajectory_evaluation_dual_process.py:
-    172-252 is the single stream being reassembled)."""
+    GPU: per step the library streams submit B new pairs as every rank does, and torch's stream -- after
+    waiting for the retired batch's records, as before the all-gather -- runs the pose tail and the serial
+    absolute chain over a whole world-N window, N x B records (stream.PoseTail / dvo_pose_tail_records), as
+    rank 0 does after the collective.  The gathered window is the retired batch's records and corners tiled
+    N times (the tail's cost does not depend on their values).  Reported: ms per step with and without the
+    rank-0 tail and the difference, against north_star's near-linear scaling (trajectory_evaluation_dual_
+    process.py:172-252 is the single stream being reassembled)."""
     import torch
     from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
     from droplet_visual_odometry_amd.stream import PoseTail
     from droplet_visual_odometry_amd.synth import MARKER_LEN
-    B, S, N = args.batch, len(fss), args.tail_world
+    B, S, N = args.batch, len(pipe.fss), args.tail_world
     dev = pool.device
     rb = PAIR_RECORD_DTYPE.itemsize
-    wrecs = [torch.cat([recs_t[k][:B * rb]] * N).contiguous() for k in range(S)]
+    wrecs = [torch.zeros(N * B * rb, dtype=torch.uint8, device=dev) for _ in range(S)]
     cp = corners[:B].repeat(N, 1, 1).contiguous()
     cc = corners[1:B + 1].repeat(N, 1, 1).contiguous()
     tail = PoseTail(K, MARKER_LEN, ctx=ctx)
@@ -598,39 +658,43 @@ def rank0_tail_leg(args, pool, fss, recs_t, corners, n_windows, K, ctx):
     T_abs = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     cur = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
+    done = [None] * S
+
+    def on_retire(k, r, pairs, s0):
+        fs = pipe.fss[k]
+        cur.wait_event(fs.record_event())  # the records are final (before the collective)
+        # stands in for the all-gather: it reads the records buffer, which the library rewrites only
+        # pipeline_depth() submits later, after waiting for this copy
+        wrecs[k][:pairs * rb].copy_(r[:pairs * rb])
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        done[k] = ev
+        tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
 
     def run(with_tail):
+        pipe.on_retire = on_retire if with_tail else (lambda *a: None)
+
         def step(i):
             s0, k = (i % n_windows) * B, i % S
-            fs = fss[k]
-            fs.wait_event(getattr(fs, "_tail_done", None))  # the slot's records were read by its last "collective"
-            fs.process(pool[s0:s0 + B + 1], recs_t[k], wait_torch=False)
-            if with_tail:
-                cur.wait_event(fs.record_event())  # the records are final (before the collective)
-                # stands in for the all-gather: it reads the send buffer, and the library waits only for it
-                wrecs[k][:B * rb].copy_(recs_t[k][:B * rb])
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                fs._tail_done = ev
-                tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
+            pipe.fss[k].wait_event(done[k])
+            pipe.step(k, pool[s0:s0 + B + 1], s0)
 
-        for i in range(args.warmup):
+        prime = max(args.warmup, pipe.prime_steps)
+        for i in range(prime):
             step(i)
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
+        pipe.sync()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(args.warmup + i)
-        for f in fss:
-            f.sync()
-        torch.cuda.synchronize()
-        for f in fss:
-            f._tail_done = None
-        return 1e3 * (time.perf_counter() - t0) / args.steps
+            step(prime + i)
+        pipe.sync()
+        dt = 1e3 * (time.perf_counter() - t0) / args.steps
+        pipe.drain()
+        pipe.sync()
+        return dt
 
     base = run(False)
     with_tail = run(True)
+    pipe.on_retire = None
     # the tail's own duration on an otherwise idle GPU (one launch of pose_tail + pose_chain over N x B records)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

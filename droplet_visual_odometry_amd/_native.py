@@ -111,6 +111,12 @@ _SIGNATURES = {
     "dvo_stream_destroy": ([_vp], None),
     "dvo_stream_process": ([_vp, _vp, _c, _i64, _c, _vp], _c),
     "dvo_stream_process_pairs": ([_vp, _vp, _c, _i64, _c, _vp], _c),
+    "dvo_pipeline_depth": ([], _c),
+    "dvo_stream_submit": ([_vp, _vp, _c, _i64, _c, _vp], _c),
+    "dvo_stream_submit_pairs": ([_vp, _vp, _c, _i64, _c, _vp], _c),
+    "dvo_stream_drain": ([_vp], _c),
+    "dvo_stream_retired": ([_vp, ctypes.POINTER(_vp), _ip, _c], _c),
+    "dvo_stream_pose_tail_batch": ([_vp, _vp, _c, _vp, _vp, _c, _d, _vp, _vp], _c),
     "dvo_stream_pair": ([_vp, _vp, _vp, _c, _c, _vp], _c),
     "dvo_stream_sync": ([_vp], _c),
     "dvo_stream_hip_stream": ([_vp], _vp),

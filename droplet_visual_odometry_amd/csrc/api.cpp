@@ -79,6 +79,22 @@ struct dvo_stream {
     dvo_pair_record* pair_rec = nullptr;
     bool fc_valid = false;
     bool last_reuse = false;  // the last call was dvo_stream_pair(reuse_prev): pyramid slot 0 holds frame 1
+    // Pair sets (dvo_stream_submit): set k holds one batch's pairs from its submit until it
+    // retires kRansacRounds - 1 submits later (or at a drain); every submit / drain step runs one
+    // merged RANSAC round in which each occupied set takes its next round.
+    struct PairSet {
+        bool used = false;
+        int round = 0;  // the round this set runs next
+        int pairs = 0;
+        dvo_pair_record* rec = nullptr;  // the caller's records of the batch
+    };
+    PairSet sets[kMaxSets];
+    int next_set = 0;  // the set the next submit fills (sets are taken in ring order)
+    int last_set = 0;  // the set of the last submitted batch (get_matches)
+    int retired = 0;   // batches retired by the last submit / drain / process call
+    int last_sub_pairs = 0;  // pairs of the last submitted batch (get_matches)
+    dvo_pair_record* retired_rec[kMaxSets] = {};
+    int retired_pairs[kMaxSets] = {};
     // profiling: event tables per in-flight call, accumulated on query
     bool profiling = false;
     std::vector<std::vector<hipEvent_t>> ev_pending;
@@ -398,10 +414,12 @@ GeomArgs stream_geom(dvo_stream* s) {
     g.rs = s->buf.rs;
     g.fprec = s->buf.fprec;
     g.dk_off = s->buf.dk_off;
+    g.a_off = s->buf.a_off;
+    g.s_off = s->buf.s_off;
     g.dk_ctl = s->buf.dk_ctl;
     g.hyp_cap = c.max_iters > 1 ? c.max_iters : 1;
     g.dk_list = s->buf.dk_list;
-    g.dk_list_cap = (int64_t)s->cfg.max_frames * g.hyp_cap;
+    g.dk_list_cap = std::max<int64_t>(round_items_bound(s->cfg.max_frames, g.hyp_cap), g.hyp_cap);
     g.E = s->buf.E;
     g.info = s->buf.info;
     g.Rt = s->buf.Rt;
@@ -409,6 +427,27 @@ GeomArgs stream_geom(dvo_stream* s) {
     g.pose_P = s->buf.pose_P;
     g.pose_cnt = s->buf.pose_cnt;
     return g;
+}
+
+// Set k's view of the per-pair geometry arrays (pairs [k F, (k + 1) F) of the stream's sets).
+GeomArgs geom_set(const GeomArgs& g, int k, int F, int64_t hc) {
+    GeomArgs o = g;
+    const int64_t p0 = (int64_t)k * F;
+    o.pts_f = g.pts_f + p0 * g.pts_stride * 4;
+    o.m_arr = g.m_arr + p0;
+    o.npts = g.npts + p0 * g.pts_stride * 4;
+    o.models = g.models + p0 * hc * 90;
+    o.nmod = g.nmod + p0 * hc;
+    o.cnt = g.cnt + p0 * hc * 10;
+    o.subsets = g.subsets + p0 * hc * 5;
+    o.rs = g.rs + p0;
+    o.E = g.E + p0 * 90;
+    o.info = g.info + p0 * 4;
+    o.Rt = g.Rt + p0 * 12;
+    o.good = g.good + p0;
+    o.pose_P = g.pose_P + p0 * 72;
+    o.pose_cnt = g.pose_cnt + p0 * 5;
+    return o;
 }
 
 // Row pitch of the internal frame slab (word-aligned rows for the byte kernels).
@@ -441,26 +480,32 @@ int stream_alloc(dvo_stream* s) {
     A(b.mq, (size_t)F * cap);
     A(b.mt, (size_t)F * cap);
     A(b.md, (size_t)F * cap);
-    A(b.nmatch, (size_t)F);
-    A(b.pts, (size_t)F * cap * 4);
-    A(b.npts, (size_t)F * cap * 4);
+    // per-pair geometry: one copy per pair set (kRansacRounds batches in flight)
+    const size_t SF = (size_t)kRansacRounds * F;
+    A(b.nmatch, SF);
+    A(b.pts, SF * cap * 4);
+    A(b.npts, SF * cap * 4);
     const size_t hc = (size_t)(s->cfg.max_iters > 1 ? s->cfg.max_iters : 1);
-    A(b.models, (size_t)F * hc * 90);
-    A(b.nmod, (size_t)F * hc);
-    A(b.rcnt, (size_t)F * hc * 10);
-    A(b.subsets, (size_t)F * hc * 5);
-    A(b.rs, (size_t)F);
-    A(b.fprec, (size_t)F * ((hc + 63) / 64) * 128 * 64);
-    A(b.dk_off, (size_t)F + 1);
+    A(b.models, SF * hc * 90);
+    A(b.nmod, SF * hc);
+    A(b.rcnt, SF * hc * 10);
+    A(b.subsets, SF * hc * 5);
+    A(b.rs, SF);
+    A(b.hdr, SF);
+    // five-point records and parked Durand-Kerner lists of one merged round
+    A(b.fprec, (size_t)std::max<int64_t>(round_blocks_bound(F, (int)hc), (int64_t)(hc + 63) / 64) * 128 * 64);
+    A(b.dk_off, SF + 1);
+    A(b.a_off, SF + 1);
+    A(b.s_off, SF + 1);
     A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
-    A(b.dk_list, (size_t)(kDkMaxPasses - 1) * F * hc);
+    A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
-    A(b.E, (size_t)F * 90);
-    A(b.info, (size_t)F * 4);
-    A(b.Rt, (size_t)F * 12);
-    A(b.good, (size_t)F);
-    A(b.pose_P, (size_t)F * 72);
-    A(b.pose_cnt, (size_t)F * 5);
+    A(b.E, SF * 90);
+    A(b.info, SF * 4);
+    A(b.Rt, SF * 12);
+    A(b.good, SF);
+    A(b.pose_P, SF * 72);
+    A(b.pose_cnt, SF * 5);
     A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
     A(s->d_carry, (size_t)28);
 #undef A
@@ -524,17 +569,80 @@ int collect_events(dvo_stream* s) {
     return DVO_OK;
 }
 
+// One merged RANSAC round: every occupied set that has rounds left takes its next one.
+int merged_round(dvo_stream* s) {
+    dvo_ctx* ctx = s->ctx;
+    RoundSpec sp{};
+    sp.nsets = kRansacRounds;
+    sp.F = s->cfg.max_frames;
+    bool any = false;
+    for (int k = 0; k < kRansacRounds; ++k) {
+        auto& st = s->sets[k];
+        const bool run = st.used && st.round < kRansacRounds;
+        sp.round[k] = run ? st.round : -1;
+        sp.npairs[k] = run ? st.pairs : 0;
+        sp.bound[k] = kRansacBounds[k];
+        any |= run;
+    }
+    if (!any) return DVO_OK;
+    HIP_TRY(launch_ransac_round(stream_geom(s), sp, s->hs));
+    for (auto& st : s->sets)
+        if (st.used && st.round < kRansacRounds) ++st.round;
+    return DVO_OK;
+}
+
+// Retire the sets whose last round has run, oldest first: E, recoverPose, the records.
+int retire_sets(dvo_stream* s) {
+    dvo_ctx* ctx = s->ctx;
+    const int F = s->cfg.max_frames;
+    const GeomArgs g = stream_geom(s);
+    // ring order from the oldest set (the one after the newest)
+    for (int j = 1; j <= kRansacRounds; ++j) {
+        const int k = (s->last_set + j) % kRansacRounds;
+        auto& st = s->sets[k];
+        if (!st.used || st.round < kRansacRounds) continue;
+        HIP_TRY(launch_retire(geom_set(g, k, F, g.hyp_cap), st.pairs, s->buf.hdr + (size_t)k * F, st.rec, s->hs));
+        s->retired_rec[s->retired] = st.rec;
+        s->retired_pairs[s->retired] = st.pairs;
+        ++s->retired;
+        s->last_rec = st.rec;
+        s->last_pairs = st.pairs;
+        s->last_has_pairs = true;
+        st = dvo_stream::PairSet{};
+    }
+    return DVO_OK;
+}
+
+bool sets_pending(const dvo_stream* s) {
+    for (const auto& st : s->sets)
+        if (st.used) return true;
+    return false;
+}
+
+// Detection of n frames, then (unless detect_only) matching of their pairs into the next pair
+// set and one merged RANSAC round; drain: rounds until every set is done, then retire them all
+// (dvo_stream_process: this batch's records are complete when the call's work is).
 int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, int pitch, dvo_pair_record* d_rec,
-               bool detect_only, int pair_step = 1) {
+               bool detect_only, int pair_step = 1, bool drain = true) {
     dvo_ctx* ctx = s->ctx;
     StreamParams P = params_of(s, d_frames, n, fstride, pitch);
     P.pair_step = pair_step;
-    const int pairs = stream_pairs(P);
+    const int pairs = detect_only ? 0 : stream_pairs(P);
     hipEvent_t* ev = nullptr;
     const int groups = orb_groups(n);
-    if (s->profiling && !detect_only && pairs >= 1) {
+    if (s->profiling && pairs >= 1) {
         int rc = acquire_events(s, groups, &ev);
         if (rc) return rc;
+    }
+    s->retired = 0;
+    s->last_has_pairs = false;  // set again when a batch retires: the pose tail reads its records
+    const int F = s->cfg.max_frames;
+    const int k = s->next_set;
+    if (pairs >= 1 && s->sets[k].used) {  // the ring is full (cannot happen in lockstep): finish its oldest
+        int rc;
+        while (s->sets[k].used && s->sets[k].round < kRansacRounds)
+            if ((rc = merged_round(s))) return rc;
+        if ((rc = retire_sets(s))) return rc;
     }
     HIP_TRY(hipMemsetAsync(s->buf.status, 0, sizeof(int32_t) * n, s->hs));
     HIP_TRY(launch_orb(P, s->hs, ev, ev && groups ? ev + 2 * DVO_NSTAGES : nullptr));
@@ -543,13 +651,36 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     s->last_frames = d_frames;
     s->last_fstride = fstride;
     s->last_pitch = pitch;
-    s->last_has_pairs = !detect_only && pairs >= 1;
-    s->last_pairs = s->last_has_pairs ? pairs : 0;
-    s->last_rec = d_rec;
-    if (!s->last_has_pairs) return DVO_OK;
-    HIP_TRY(launch_match(P, s->cfg.cross_check, s->hs, ev));
-    GeomArgs g = stream_geom(s);
-    HIP_TRY(launch_geometry(P, g, d_rec, s->hs, ev));
+    s->last_sub_pairs = pairs;
+    if (detect_only) return DVO_OK;
+    if (pairs >= 1) {
+        // match into set k (its KeyPoint_convert points and counts), the frame-side record values
+        StreamParams Pk = P;
+        Pk.buf.pts += (size_t)k * F * s->plan.kp_cap * 4;
+        Pk.buf.nmatch += (size_t)k * F;
+        HIP_TRY(launch_match(Pk, s->cfg.cross_check, s->hs, ev));
+        HIP_TRY(launch_pair_header(P, s->buf.hdr + (size_t)k * F, s->hs));
+        const GeomArgs g = stream_geom(s);
+        HIP_TRY(launch_geometry_args(geom_set(g, k, F, g.hyp_cap), pairs, kStageNormalize, s->hs));
+        s->sets[k] = dvo_stream::PairSet{true, 0, pairs, d_rec};
+        s->last_set = k;
+        s->next_set = (k + 1) % kRansacRounds;
+    }
+    if (pairs < 1 && !drain) return DVO_OK;
+    int rc;
+    mark(ev, 6, 0, s->hs);
+    if ((rc = merged_round(s))) return rc;
+    if (drain)
+        while (sets_pending(s)) {
+            bool left = false;
+            for (const auto& st : s->sets) left |= st.used && st.round < kRansacRounds;
+            if (!left) break;
+            if ((rc = merged_round(s))) return rc;
+        }
+    mark(ev, 6, 1, s->hs);
+    mark(ev, 7, 0, s->hs);
+    if ((rc = retire_sets(s))) return rc;
+    mark(ev, 7, 1, s->hs);
     mark(ev, 8, 0, s->hs);  // pose-tail pair defaults to 0 ms; dvo_stream_pose_tail re-records it
     mark(ev, 8, 1, s->hs);
     return DVO_OK;
@@ -679,16 +810,25 @@ int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const doub
                          double marker_length, double* d_T_rel, double* d_T_abs) {
     if (!s) return DVO_EINVAL;
     dvo_ctx* ctx = s->ctx;
+    if (!s->last_has_pairs) return fail(ctx, DVO_EINVAL, "pose tail needs a preceding dvo_stream_process");
+    return dvo_stream_pose_tail_batch(s, s->last_rec, s->last_pairs, d_corners_prev, d_corners_cur, k, marker_length,
+                                      d_T_rel, d_T_abs);
+}
+
+int dvo_stream_pose_tail_batch(dvo_stream* s, const dvo_pair_record* d_records, int pairs, const double* d_corners_prev,
+                               const double* d_corners_cur, int k, double marker_length, double* d_T_rel,
+                               double* d_T_abs) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
     if (k < 2 || !d_corners_prev || !d_corners_cur || !d_T_rel || !d_T_abs)
         return fail(ctx, DVO_EINVAL, "pose tail needs >= 2 corners per frame and output buffers");
-    if (!s->last_has_pairs) return fail(ctx, DVO_EINVAL, "pose tail needs a preceding dvo_stream_process");
-    const int pairs = s->last_pairs;
+    if (!d_records || pairs < 1) return fail(ctx, DVO_EINVAL, "pose tail needs records");
     HIP_TRY(hipSetDevice(ctx->device));
     hipEvent_t* ev = (s->profiling && !s->ev_pending.empty()) ? s->ev_pending.back().data() : nullptr;
     dvo_stream* o = s->carry_owner;  // pose tails on one carry run in call order, across streams
     if (o->carry_ev_valid) HIP_TRY(hipStreamWaitEvent(s->hs, o->carry_ev, 0));
     mark(ev, 8, 0, s->hs);
-    HIP_TRY(launch_pose_tail(s->last_rec, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
+    HIP_TRY(launch_pose_tail(d_records, pairs, s->cfg.K, d_corners_prev, d_corners_cur, k, marker_length,
                              o->d_carry, d_T_rel, d_T_abs, s->hs));
     mark(ev, 8, 1, s->hs);
     HIP_TRY(hipEventRecord(o->carry_ev, s->hs));
@@ -742,7 +882,7 @@ int dvo_stream_stage_times(dvo_stream* s, double* ms, int* calls) {
 void* dvo_stream_hip_stream(dvo_stream* s) { return s ? (void*)s->hs : nullptr; }
 
 static int process_frames(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
-                   dvo_pair_record* d_records, int pair_step) {
+                   dvo_pair_record* d_records, int pair_step, bool drain = true) {
     dvo_ctx* ctx = s->ctx;
     if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -752,9 +892,10 @@ static int process_frames(dvo_stream* s, const uint8_t* d_frames, int n_frames, 
         for (int i = 0; i < n_frames; ++i)
             HIP_TRY(hipMemcpy2DAsync(s->d_frames + (size_t)i * pw * s->cfg.height, pw, d_frames + i * frame_stride,
                                      stride, s->cfg.width, s->cfg.height, hipMemcpyDeviceToDevice, s->hs));
-        return run_stream(s, s->d_frames, n_frames, (int64_t)pw * s->cfg.height, pw, d_records, false, pair_step);
+        return run_stream(s, s->d_frames, n_frames, (int64_t)pw * s->cfg.height, pw, d_records, false, pair_step,
+                          drain);
     }
-    return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false, pair_step);
+    return run_stream(s, d_frames, n_frames, frame_stride, stride, d_records, false, pair_step, drain);
 }
 
 int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
@@ -764,6 +905,51 @@ int dvo_stream_process(dvo_stream* s, const uint8_t* d_frames, int n_frames, int
     if (n_frames < 1 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range");
     if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
     return process_frames(s, d_frames, n_frames, frame_stride, stride, d_records, 1);
+}
+
+int dvo_pipeline_depth(void) { return kRansacRounds; }
+
+int dvo_stream_submit(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                      dvo_pair_record* d_records) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (n_frames < 2 || n_frames > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_frames out of range (2..max)");
+    if (!d_records) return fail(ctx, DVO_EINVAL, "null records");
+    return process_frames(s, d_frames, n_frames, frame_stride, stride, d_records, 1, false);
+}
+
+int dvo_stream_submit_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
+                            dvo_pair_record* d_records) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    if (n_pairs < 1 || 2 * (int64_t)n_pairs > s->cfg.max_frames) return fail(ctx, DVO_EINVAL, "n_pairs out of range");
+    if (!d_records) return fail(ctx, DVO_EINVAL, "null records");
+    return process_frames(s, d_frames, 2 * n_pairs, frame_stride, stride, d_records, 2, false);
+}
+
+int dvo_stream_drain(dvo_stream* s) {
+    if (!s) return DVO_EINVAL;
+    dvo_ctx* ctx = s->ctx;
+    HIP_TRY(hipSetDevice(ctx->device));
+    s->retired = 0;
+    s->last_has_pairs = false;
+    int rc;
+    for (;;) {
+        bool left = false;
+        for (const auto& st : s->sets) left |= st.used && st.round < kRansacRounds;
+        if (!left) break;
+        if ((rc = merged_round(s))) return rc;
+    }
+    return retire_sets(s);
+}
+
+int dvo_stream_retired(dvo_stream* s, void** records, int* pairs, int cap) {
+    if (!s || (cap > 0 && (!records || !pairs))) return DVO_EINVAL;
+    for (int i = 0; i < s->retired && i < cap; ++i) {
+        records[i] = s->retired_rec[i];
+        pairs[i] = s->retired_pairs[i];
+    }
+    return s->retired;
 }
 
 int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
@@ -791,6 +977,7 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     if (s->cfg.max_frames < 2) return fail(ctx, DVO_EINVAL, "dvo_stream_pair needs max_frames >= 2");
     if (!cur_img || !rec_out || stride < w || (!reuse_prev && !prev_img)) return fail(ctx, DVO_EINVAL, "bad image buffer");
     if (reuse_prev && !s->fc_valid) return fail(ctx, DVO_EINVAL, "reuse_prev needs a preceding dvo_stream_pair");
+    if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "dvo_stream_pair: submitted batches are pending (dvo_stream_drain)");
     // the feature cache is valid only after a call that succeeds (a failing call may have left
     // its frame half-way through the rotation)
     s->fc_valid = false;
@@ -869,6 +1056,8 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     s->last_reuse = reuse_prev != 0;
     s->last_nframes = 2;
     s->last_pairs = 1;
+    s->last_sub_pairs = 1;
+    s->last_set = 0;
     s->last_has_pairs = true;
     s->last_rec = s->pair_rec;
     s->last_frames = s->d_frames;
@@ -910,10 +1099,11 @@ int dvo_stream_get_features(dvo_stream* s, int frame, dvo_keypoint* kps, uint8_t
 int dvo_stream_get_matches(dvo_stream* s, int pair, dvo_dmatch* out, int cap, int* m) {
     if (!s || !m) return DVO_EINVAL;
     dvo_ctx* ctx = s->ctx;
-    if (pair < 0 || pair >= s->last_pairs) return fail(ctx, DVO_EINVAL, "pair out of range");
+    if (pair < 0 || pair >= s->last_sub_pairs) return fail(ctx, DVO_EINVAL, "pair out of range");
     HIP_TRY(hipStreamSynchronize(s->hs));
     int nm = 0;
-    HIP_TRY(hipMemcpy(&nm, s->buf.nmatch + pair, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nm, s->buf.nmatch + (size_t)s->last_set * s->cfg.max_frames + pair, sizeof(int),
+                      hipMemcpyDeviceToHost));
     *m = nm;
     if (nm > cap) return fail(ctx, DVO_ECAP, "caller capacity too small");
     std::vector<int32_t> q(nm), t(nm);
@@ -1507,7 +1697,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     if (!(prob > 0 && prob < 1)) return fail(ctx, DVO_EINVAL, "prob must be in (0, 1)");
     if (m < 5) return fail(ctx, DVO_EFEWPTS, "fewer than 5 correspondences");
     HIP_TRY(hipSetDevice(ctx->device));
-    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *drec, *doff, *dctl, *dlist;
+    void *dpts, *dn, *dmod, *dE, *dinfo, *dmask, *dnmod, *dcnt, *dsub, *drs, *drec, *doff, *dctl, *dlist, *daoff, *dsoff;
     int rc;
     const size_t hc = (size_t)(max_iters > 1 ? max_iters : 1);
     Staging st;
@@ -1521,6 +1711,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
         (rc = scratch(ctx, 23, 4 * (2 + kDkMaxPasses), &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
+        (rc = scratch(ctx, 62, 8, &daoff)) || (rc = scratch(ctx, 63, 8, &dsoff)) ||
         (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
         return rc;
     GeomArgs g{};
@@ -1542,6 +1733,8 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
     g.rs = (RansacState*)drs;
     g.fprec = (double*)drec;
     g.dk_off = (int32_t*)doff;
+    g.a_off = (int32_t*)daoff;
+    g.s_off = (int32_t*)dsoff;
     g.dk_ctl = (int32_t*)dctl;
     g.dk_list = (int32_t*)dlist;
     g.dk_list_cap = (int64_t)hc;

@@ -96,13 +96,33 @@ struct RansacState {
     int32_t pad[2];
 };
 constexpr int kDkMaxPasses = 4;  // Durand-Kerner passes per round (geometry.hip kDkBudgets)
-// RANSAC rounds: round r solves hypotheses [bound[r-1], min(bound[r], niters)).
+// RANSAC rounds of a stream batch: round r solves hypotheses [bound[r-1], min(bound[r], niters)),
+// the last round everything left.  A batch's pairs take one round per dvo_stream_submit call
+// (the rounds of kRansacRounds consecutive batches run as ONE merged launch sequence), so a
+// round costs no extra Durand-Kerner tail; dvo_stream_process runs them back to back.
+// Hypotheses solved per pair at 1280x720 / 2000 features (oracle replay, tools/ransac_schedule_sim.py,
+// profiles/r05c_*): 64 | rest 177.8, 32 | 64 | 128 | 256 | rest 141.9, for 132.2 iterations used.
 #ifndef DVO_RANSAC_BOUNDS
-#define DVO_RANSAC_BOUNDS 64, 1 << 30
+#define DVO_RANSAC_BOUNDS 32, 64, 128, 256
 #endif
-constexpr int kRansacBounds[] = {DVO_RANSAC_BOUNDS};
+constexpr int kRansacBounds[] = {DVO_RANSAC_BOUNDS, 1 << 30};
 constexpr int kRansacRounds = sizeof(kRansacBounds) / sizeof(int);
-constexpr int kRansacRound1 = kRansacBounds[0];  // hypotheses per pair in round 1
+constexpr int kMaxSets = 8;  // pair sets (batches in flight) of a merged round
+static_assert(kRansacRounds <= kMaxSets, "one pair set per round in flight");
+// One merged RANSAC round: launch pairs [0, nsets F) are nsets sets of F pairs (set k = pairs
+// [k F, (k + 1) F), one stream batch each); set k runs round[k] (-1: idle) over its first
+// npairs[k] pairs.  Round 0 starts a set's pairs (RNG, niters = maxIters).
+struct RoundSpec {
+    int nsets, F;
+    int round[kMaxSets];
+    int npairs[kMaxSets];
+    int bound[kMaxSets];  // hypotheses bound of round r (the last: 1 << 30)
+};
+// Per-pair values the record needs from the frames (records_kernel), kept with the pair's set
+// because the frames' buffers are rewritten by the next batch before the set retires.
+struct PairHeader {
+    int32_t nkp_prev, nkp_cur, flags, pad;
+};
 
 struct Buffers {
     uint8_t* pyr;
@@ -123,25 +143,29 @@ struct Buffers {
     int32_t* mq;          // [F][kp_cap] match queryIdx (sorted by (dist, q))
     int32_t* mt;          // [F][kp_cap] match trainIdx
     float* md;            // [F][kp_cap] match distance
-    int32_t* nmatch;      // [F]
-    float* pts;           // [F][kp_cap][4] (x1, y1, x2, y2) KeyPoint_convert pixel coords
-    double* npts;         // [F][kp_cap][4] normalised coords for RANSAC / recoverPose
-    double* models;       // [F][hyp_cap][10][9]
-    int32_t* nmod;        // [F][hyp_cap]
-    int32_t* rcnt;        // [F][hyp_cap][10]
-    int32_t* subsets;     // [F][hyp_cap][5]
-    RansacState* rs;      // [F]
-    double* fprec;        // [F][ceil(hyp_cap / 64)][128][64]
-    int32_t* dk_off;      // [F + 1]
+    int32_t* nmatch;      // [sets F]
+    // per pair, one copy per pair set ([sets][F] pairs: a set holds one batch until it retires)
+    float* pts;           // [sets F][kp_cap][4] (x1, y1, x2, y2) KeyPoint_convert pixel coords
+    double* npts;         // [sets F][kp_cap][4] normalised coords for RANSAC / recoverPose
+    double* models;       // [sets F][hyp_cap][10][9]
+    int32_t* nmod;        // [sets F][hyp_cap]
+    int32_t* rcnt;        // [sets F][hyp_cap][10]
+    int32_t* subsets;     // [sets F][hyp_cap][5]
+    RansacState* rs;      // [sets F]
+    double* fprec;        // [round blocks][128][64] five-point records of one round (a_off)
+    int32_t* dk_off;      // [sets F + 1] round work list: hypotheses before each pair
+    int32_t* a_off;       // [sets F + 1] 64-hypothesis blocks before each pair (stage A / C, records)
+    int32_t* s_off;       // [sets F + 1] score blocks before each pair
+    PairHeader* hdr;      // [sets][F]
     int32_t* dk_ctl;      // [2 + kDkMaxPasses]
     int32_t* dk_list;     // [kDkMaxPasses - 1][F * hyp_cap] parked Durand-Kerner polynomials
     int32_t* status;      // [F] per-frame error flags
-    double* E;            // [F][90]
-    int32_t* info;        // [F][4] rows, inliers, iters, status
-    double* Rt;           // [F][12]
-    int32_t* good;        // [F]
-    double* pose_P;       // [F][72] recoverPose decompositions (4 P, R1, R2, t)
-    int32_t* pose_cnt;    // [F][5] decomposition valid flag, cheirality counts
+    double* E;            // [sets F][90]
+    int32_t* info;        // [sets F][4] rows, inliers, iters, status
+    double* Rt;           // [sets F][12]
+    int32_t* good;        // [sets F]
+    double* pose_P;       // [sets F][72] recoverPose decompositions (4 P, R1, R2, t)
+    int32_t* pose_cnt;    // [sets F][5] decomposition valid flag, cheirality counts
 };
 
 
@@ -197,8 +221,10 @@ struct GeomArgs {
     int32_t* cnt;           // [pairs][hyp_cap][10] inlier counts
     int32_t* subsets;       // [pairs][hyp_cap][5] sampled point indices
     RansacState* rs;        // [pairs]
-    double* fprec;          // [pairs][ceil(hyp_cap / 64)][128][64] five-point records
+    double* fprec;          // [round blocks][128][64] five-point records of the round (block = a_off[p] + (h - h0) / 64)
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
+    int32_t* a_off;         // [pairs + 1] 64-hypothesis blocks of the round before each pair
+    int32_t* s_off;         // [pairs + 1] score blocks of the round before each pair
     int32_t* dk_ctl;        // [2 + kDkMaxPasses] -, pass-0 items, parked after pass k
     int32_t* dk_list;       // [kDkMaxPasses - 1][dk_list_cap] parked polynomials (work-list items)
     int64_t dk_list_cap;    // >= pairs * hyp_cap
@@ -215,7 +241,7 @@ struct GeomArgs {
     int32_t* pose_cnt;      // [pairs][5] valid flag, cheirality counts of the 4 decompositions
 };
 
-constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4;
+constexpr int kStageNormalize = 1, kStageRansac = 2, kStagePose = 4, kStageFinish = 16;
 // kStageOneRound: the per-call findEssentialMat (one pair): a single RANSAC round
 // over every hypothesis up to maxIters, solved with one lane per root.  Stream
 // batches keep the two-round schedule, so their records (n_hypotheses) do not
@@ -309,6 +335,15 @@ hipError_t launch_match(const StreamParams& P, int cross_check, hipStream_t s, h
 hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_record* records, hipStream_t s,
                            hipEvent_t* ev = nullptr, bool one_round = false);
 hipError_t launch_geometry_args(const GeomArgs& g, int pairs, int stages, hipStream_t s);
+// Stream batches (api.cpp dvo_stream_submit): the per-set pieces.  g_all spans every set (pairs
+// [0, nsets F)); g_set is one set's view (geom_set).
+hipError_t launch_pair_header(const StreamParams& P, PairHeader* hdr, hipStream_t s);
+hipError_t launch_ransac_round(const GeomArgs& g_all, const RoundSpec& spec, hipStream_t s);
+hipError_t launch_retire(const GeomArgs& g_set, int pairs, const PairHeader* hdr, dvo_pair_record* records,
+                         hipStream_t s);
+// five-point record blocks a merged round can need (sizes Buffers::fprec, dk_list)
+int64_t round_blocks_bound(int F, int hyp_cap);
+int64_t round_items_bound(int F, int hyp_cap);
 // Undistortion (undistort.hip): camera K, distortion k1 k2 p1 p2 k3 k4 k5 k6 s1..s4.
 struct UndistortGeom {
     int w, h, stripe;

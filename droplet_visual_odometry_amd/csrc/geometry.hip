@@ -1057,16 +1057,26 @@ __device__ __forceinline__ uint64_t mwc_mont(uint64_t a, uint64_t bR) {  // a * 
     const bool c2 = t2 < t;
     return (c1 || c2 || t2 >= kMwcM) ? t2 - kMwcM : t2;
 }
-__global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs, int round, int bound) {
+// Launch pair p belongs to set p / F, which runs round spec.round[set] (-1: idle set, its pairs
+// get an empty range); slots past the set's batch (npairs) start with m = 0 (nothing to do).
+__global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, RoundSpec spec) {
     const int p = blockIdx.x;
-    if (p >= pairs) return;
+    const int set = p / spec.F, local = p - set * spec.F;
+    if (set >= spec.nsets) return;
     const int lane = threadIdx.x;
     __shared__ uint64_t s_st[kSampleBuf];
     RansacState S = g.rs[p];
     int32_t* idx = g.subsets + (int64_t)p * g.hyp_cap * 5;
+    const int round = spec.round[set];
+    if (round < 0) {  // idle set: no hypotheses this launch
+        S.h0 = S.h1;
+        if (lane == 0) g.rs[p] = S;
+        return;
+    }
+    const int bound = spec.bound[round];
     int h0, h1;
     if (round == 0) {
-        S.m = pair_m(g, p);
+        S.m = local < spec.npairs[set] ? pair_m(g, p) : 0;
         S.rng = ~0ull;  // RNG rng((uint64)-1)
         S.niters = g.max_iters > 1 ? g.max_iters : 1;
         S.iter = 0;
@@ -1176,49 +1186,85 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, int pairs
     if (lane == 0) g.rs[p] = S;
 }
 
+// The five-point record of hypothesis h of launch pair p: records exist for the round's
+// hypotheses only, 64 per block, the pair's [h0, h1) from block a_off[p] on (so a stage A / C
+// block of 64 consecutive hypotheses writes one record block: coalesced).
 __device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
-    const int nblk = (g.hyp_cap + 63) >> 6;
-    return g.fprec + ((int64_t)(p * nblk + (h >> 6)) * kRecDoubles) * 64 + (h & 63);
+    const int64_t r = (int64_t)g.a_off[p] * 64 + (h - g.rs[p].h0);
+    return g.fprec + ((r >> 6) * kRecDoubles) * 64 + (r & 63);
+}
+
+// Pair of a round work-list item: the p with off[p] <= item < off[p + 1] (off ascending).
+__device__ __forceinline__ int pair_of(const int32_t* off, int pairs, int item) {
+    int lo = 0, hi = pairs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= item) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 // Work list of the round for the Durand-Kerner kernel: exclusive prefix of the
 // per-pair hypothesis counts, the total, and a reset queue head.
-__global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs) {
-    __shared__ int s_sum[1024];
-    __shared__ int s_carry;
-    if (threadIdx.x == 0) s_carry = 0;
+// and the same prefixes in 64-hypothesis blocks (stage A / C, five-point records) and in score
+// blocks of sh hypotheses.  Wave prefix sums, one carry per 1024 pairs.
+__global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs, int sh) {
+    __shared__ int4 s_w[16];
+    __shared__ int4 s_carry;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = make_int4(0, 0, 0, 0);
     for (int b0 = 0; b0 < pairs; b0 += 1024) {
         const int p = b0 + threadIdx.x;
         const int n = p < pairs ? max(0, g.rs[p].h1 - g.rs[p].h0) : 0;
-        __syncthreads();
-        s_sum[threadIdx.x] = n;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-            const int v = threadIdx.x >= off ? s_sum[threadIdx.x - off] : 0;
-            __syncthreads();
-            s_sum[threadIdx.x] += v;
-            __syncthreads();
+        const int na = (n + 63) >> 6, ns = (n + sh - 1) / sh;
+        int x = n, y = na, z = ns;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans
+            const int xo = __shfl_up(x, o), yo = __shfl_up(y, o), zo = __shfl_up(z, o);
+            if (lane >= o) {
+                x += xo;
+                y += yo;
+                z += zo;
+            }
         }
-        if (p < pairs) g.dk_off[p] = s_carry + s_sum[threadIdx.x] - n;
         __syncthreads();
-        if (threadIdx.x == 1023) s_carry += s_sum[1023];
+        if (lane == 63) s_w[wid] = make_int4(x, y, z, 0);
+        __syncthreads();
+        int4 c = s_carry;
+        for (int w = 0; w < wid; ++w) {
+            c.x += s_w[w].x;
+            c.y += s_w[w].y;
+            c.z += s_w[w].z;
+        }
+        if (p < pairs) {
+            g.dk_off[p] = c.x + x - n;
+            g.a_off[p] = c.y + y - na;
+            g.s_off[p] = c.z + z - ns;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = make_int4(c.x + x, c.y + y, c.z + z, 0);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        g.dk_off[pairs] = s_carry;
+        g.dk_off[pairs] = s_carry.x;
+        g.a_off[pairs] = s_carry.y;
+        g.s_off[pairs] = s_carry.z;
         g.dk_ctl[0] = 0;
-        g.dk_ctl[1] = s_carry;  // pass 0 items
+        g.dk_ctl[1] = s_carry.x;  // pass 0 items
         for (int k = 0; k < kDkMaxPasses; ++k) g.dk_ctl[2 + k] = 0;  // parked after pass k
     }
 }
 
 // Stage A of every hypothesis of the round (one thread each).
-__global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g) {
-    const int p = blockIdx.y;
+// A 1-D grid over the round's 64-hypothesis blocks (a_off), sized for the largest round.
+__global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g, int pairs) {
+    const int b = blockIdx.x;
+    if (b >= g.a_off[pairs]) return;
+    const int p = pair_of(g.a_off, pairs, b);
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
-    const int h = h0 + blockIdx.x * kSolveNT + threadIdx.x;
-    if (h0 + (int)blockIdx.x * kSolveNT >= h1) return;
+    const int h = h0 + (b - g.a_off[p]) * kSolveNT + threadIdx.x;
     __shared__ double lds_g[36 * kSolveNT];
     if (h >= h1) return;
     const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
@@ -1297,12 +1343,7 @@ void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
     const int e = blockIdx.x * kDkNT + threadIdx.x;
     if (e >= total) return;
     const int item = pass == 0 ? e : g.dk_list[(int64_t)(pass - 1) * g.dk_list_cap + e];
-    int lo = 0, hi = pairs - 1;  // pair p with off[p] <= item < off[p + 1]
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (g.dk_off[mid] <= item) lo = mid;
-        else hi = mid - 1;
-    }
+    const int lo = pair_of(g.dk_off, pairs, item);
     double* R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
     if (pass == 0 && R[kRecGeneric * 64] != 0.0) return;  // stage C runs the generic solver
     double c[11];
@@ -1403,12 +1444,7 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
     bool active = item < total;
     double* R = nullptr;
     if (active) {
-        int lo = 0, hi = pairs - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (g.dk_off[mid] <= item) lo = mid;
-            else hi = mid - 1;
-        }
+        const int lo = pair_of(g.dk_off, pairs, item);
         R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
         active = R[kRecGeneric * 64] == 0.0;  // else stage C runs the generic solver
     }
@@ -1479,11 +1515,13 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
 }
 
 // Stage C of every hypothesis of the round: models and their count.
-__global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g) {
-    const int p = blockIdx.y;
+__global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g, int pairs) {
+    const int b = blockIdx.x;
+    if (b >= g.a_off[pairs]) return;
+    const int p = pair_of(g.a_off, pairs, b);
     const RansacState& S = g.rs[p];
     const int h0 = S.h0, h1 = S.h1;
-    const int h = h0 + blockIdx.x * kSolveNT + threadIdx.x;
+    const int h = h0 + (b - g.a_off[p]) * kSolveNT + threadIdx.x;
     if (h >= h1) return;
     g.nmod[(int64_t)p * g.hyp_cap + h] =
         fp_stage_c(hyp_record(g, p, h), g.models + ((int64_t)p * g.hyp_cap + h) * 90);
@@ -1560,10 +1598,12 @@ __global__ __launch_bounds__(64) void ransac_stage_c_row_kernel(GeomArgs g) {
 // HYPS = kScoreHyps for batches; the per-call path (one pair) takes kScoreHypsCall
 // so that its few blocks spread over more CUs (fewer models per wave in sequence).
 template <int HYPS>
-__global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g) {
-    const int p = blockIdx.y;
+__global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g, int pairs) {
+    const int b = blockIdx.x;
+    if (b >= g.s_off[pairs]) return;
+    const int p = pair_of(g.s_off, pairs, b);
     const RansacState& S = g.rs[p];
-    const int hb = S.h0 + blockIdx.x * HYPS;
+    const int hb = S.h0 + (b - g.s_off[p]) * HYPS;
     if (hb >= S.h1 || S.m <= 5) return;
     const int hn = min(HYPS, S.h1 - hb);
     const int m = S.m;
@@ -1872,45 +1912,100 @@ __global__ __launch_bounds__(256) void ransac_finish_kernel(GeomArgs g) {
     }
 }
 
-// one = kStageOneRound (the per-call path): a single pair leaves the GPU idle,
-// so it takes one round over every hypothesis up to maxIters -- one
-// Durand-Kerner tail instead of two -- solved by ransac_dk_wide_kernel.
-// Rounds only schedule the same hypotheses; the replay's result is the same.
-hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) {
-    const int cap = g.hyp_cap;
-    const int rounds = one ? 1 : kRansacRounds;
-    for (int round = 0; round < rounds; ++round) {
-        const int hi = one ? cap : kRansacBounds[round];
-        const int lo = round == 0 ? 0 : kRansacBounds[round - 1];
-        const int span = min(hi, cap) - lo;
-        if (span <= 0) break;
-        hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, pairs, round, hi);
-        const dim3 hgrid((span + kSolveNT - 1) / kSolveNT, pairs);
-        hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs);
-        hipLaunchKernelGGL(ransac_stage_a_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        if (one) {
-            hipLaunchKernelGGL(ransac_dk_wide_kernel, dim3((unsigned)(((int64_t)pairs * span + 3) / 4)), dim3(64), 0, s, g,
-                               pairs);
-        } else {
-            const dim3 dgrid((unsigned)(((int64_t)pairs * span + kDkNT - 1) / kDkNT));
-            for (int pass = 0; pass < kDkPasses; ++pass)
-                hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
-                                   pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
+// Upper bounds of one round's work (host): the hypotheses a set at round r can take are
+// [bound[r-1], bound[r]) clamped to the cap, so the grids of a launch are sized from its spec.
+struct RoundWork {
+    int64_t items, ablocks, sblocks;
+};
+static RoundWork round_work(const RoundSpec& spec, int cap, int sh) {
+    RoundWork w{0, 0, 0};
+    for (int k = 0; k < spec.nsets; ++k) {
+        const int r = spec.round[k];
+        if (r < 0) continue;
+        const int lo = r == 0 ? 0 : min(spec.bound[r - 1], cap), hi = min(spec.bound[r], cap);
+        const int span = max(0, hi - lo);
+        w.items += (int64_t)spec.npairs[k] * span;
+        w.ablocks += (int64_t)spec.npairs[k] * ((span + 63) / 64);
+        w.sblocks += (int64_t)spec.npairs[k] * ((span + sh - 1) / sh);
+    }
+    return w;
+}
+
+// A stream's round of the largest total work: one set at each round (Buffers::fprec, dk_list).
+static RoundSpec full_spec(int F) {
+    RoundSpec sp{};
+    sp.nsets = kRansacRounds;
+    sp.F = F;
+    for (int r = 0; r < kRansacRounds; ++r) {
+        sp.round[r] = r;
+        sp.npairs[r] = F;
+        sp.bound[r] = kRansacBounds[r];
+    }
+    return sp;
+}
+int64_t round_blocks_bound(int F, int hyp_cap) { return round_work(full_spec(F), hyp_cap, kScoreHyps).ablocks; }
+int64_t round_items_bound(int F, int hyp_cap) { return round_work(full_spec(F), hyp_cap, kScoreHyps).items; }
+
+// One RANSAC round over the launch pairs [0, nsets F): sample -> plan -> stage A ->
+// Durand-Kerner -> stage C -> score -> replay.  one (the per-call path, kStageOneRound): a
+// single pair leaves the GPU idle, so it takes one round over every hypothesis up to maxIters
+// (one Durand-Kerner tail instead of several), solved with one lane per root
+// (ransac_dk_wide_kernel), stage C by rows, and small score blocks.  Rounds only schedule the
+// same hypotheses; the replay's result is the same.
+static hipError_t launch_round(const GeomArgs& g, const RoundSpec& spec, bool one, hipStream_t s) {
+    const int pairs = spec.nsets * spec.F;
+    if (pairs <= 0) return hipSuccess;
+    const int sh = one ? kScoreHypsCall : kScoreHyps;
+    const RoundWork w = round_work(spec, g.hyp_cap, sh);
+    hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, spec);
+    if (w.items == 0) return hipGetLastError();  // no pair of the launch can have a hypothesis
+    hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs, sh);
+    hipLaunchKernelGGL(ransac_stage_a_kernel, dim3((unsigned)w.ablocks), dim3(kSolveNT), 0, s, g, pairs);
+    if (one) {
+        hipLaunchKernelGGL(ransac_dk_wide_kernel, dim3((unsigned)((w.items + 3) / 4)), dim3(64), 0, s, g, pairs);
+        int span = 0;  // the per-call path: one set, round 0 up to the cap
+        for (int k = 0; k < spec.nsets; ++k) span = max(span, min(spec.bound[0], g.hyp_cap));
+        hipLaunchKernelGGL(ransac_stage_c_row_kernel, dim3((span + 3) / 4, pairs), dim3(64), 0, s, g);
+        hipLaunchKernelGGL(ransac_score_kernel<kScoreHypsCall>, dim3((unsigned)w.sblocks), dim3(kScoreNT), 0, s, g,
+                           pairs);
+    } else {
+        const dim3 dgrid((unsigned)((w.items + kDkNT - 1) / kDkNT));
+        for (int pass = 0; pass < kDkPasses; ++pass)
+            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
+                               pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
 #ifdef DVO_DK_STATS
-            hipLaunchKernelGGL(dk_stats_kernel, dim3(1), dim3(1), 0, s, round, (int)dgrid.x * (kDkNT / 64));
+        hipLaunchKernelGGL(dk_stats_kernel, dim3(1), dim3(1), 0, s, spec.round[0], (int)dgrid.x * (kDkNT / 64));
 #endif
+        hipLaunchKernelGGL(ransac_stage_c_kernel, dim3((unsigned)w.ablocks), dim3(kSolveNT), 0, s, g, pairs);
+        hipLaunchKernelGGL(ransac_score_kernel<kScoreHyps>, dim3((unsigned)w.sblocks), dim3(kScoreNT), 0, s, g,
+                           pairs);
+    }
+    hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
+    return hipGetLastError();
+}
+
+hipError_t launch_ransac_round(const GeomArgs& g_all, const RoundSpec& spec, hipStream_t s) {
+    return launch_round(g_all, spec, false, s);
+}
+
+// Every round of a batch of `pairs` back to back (one set), then E and info.
+static hipError_t launch_ransac(const GeomArgs& g, int pairs, bool one, hipStream_t s) {
+    RoundSpec sp{};
+    sp.nsets = 1;
+    sp.F = pairs;
+    sp.npairs[0] = pairs;
+    if (one) {
+        sp.round[0] = 0;
+        sp.bound[0] = 1 << 30;
+        hipError_t e = launch_round(g, sp, true, s);
+        if (e != hipSuccess) return e;
+    } else {
+        for (int r = 0; r < kRansacRounds; ++r) sp.bound[r] = kRansacBounds[r];
+        for (int r = 0; r < kRansacRounds; ++r) {
+            sp.round[0] = r;
+            hipError_t e = launch_round(g, sp, false, s);
+            if (e != hipSuccess) return e;
         }
-        if (one)
-            hipLaunchKernelGGL(ransac_stage_c_row_kernel, dim3((span + 3) / 4, pairs), dim3(64), 0, s, g);
-        else
-            hipLaunchKernelGGL(ransac_stage_c_kernel, hgrid, dim3(kSolveNT), 0, s, g);
-        if (one)
-            hipLaunchKernelGGL(ransac_score_kernel<kScoreHypsCall>,
-                               dim3((span + kScoreHypsCall - 1) / kScoreHypsCall, pairs), dim3(kScoreNT), 0, s, g);
-        else
-            hipLaunchKernelGGL(ransac_score_kernel<kScoreHyps>, dim3((span + kScoreHyps - 1) / kScoreHyps, pairs),
-                               dim3(kScoreNT), 0, s, g);
-        hipLaunchKernelGGL(ransac_replay_kernel, dim3(pairs), dim3(kReplayNT), 0, s, g);
     }
     hipLaunchKernelGGL(ransac_finish_kernel, dim3(pairs), dim3(256), 0, s, g);
     return hipGetLastError();
@@ -2110,29 +2205,35 @@ __global__ void triangulate_kernel(const double* P, const double* x, int k, doub
     for (int r = 0; r < 4; ++r) X[r * k + i] = out[r];
 }
 
-__global__ void records_kernel(StreamParams P, GeomArgs g, dvo_pair_record* rec) {
+// The frame-side values of each pair's record, kept with the pair's set (PairHeader).
+__global__ void pair_header_kernel(StreamParams P, PairHeader* hdr) {
     const int p = blockIdx.x * 64 + threadIdx.x;
     if (p >= stream_pairs(P)) return;
     const int fp = pair_frame(P, p);  // the pair's frames are fp, fp + 1
+    hdr[p] = PairHeader{P.buf.nkp[fp], P.buf.nkp[fp + 1], P.buf.status[fp] | P.buf.status[fp + 1], 0};
+}
+
+__global__ void records_kernel(GeomArgs g, const PairHeader* hdr, int pairs, dvo_pair_record* rec) {
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= pairs) return;
     dvo_pair_record r;
     const int32_t* info = g.info + (int64_t)p * 4;
     const double* E = g.E + (int64_t)p * 90;
     const double* Rt = g.Rt + (int64_t)p * 12;
+    const PairHeader h = hdr[p];
     const bool ok = info[3] == DVO_OK && info[0] == 3;
     for (int k = 0; k < 9; ++k) r.R[k] = ok ? Rt[k] : 0.0;
     for (int k = 0; k < 3; ++k) r.t[k] = ok ? Rt[9 + k] : 0.0;
     for (int k = 0; k < 9; ++k) r.E[k] = info[0] >= 3 ? E[k] : 0.0;
-    r.n_kp_prev = P.buf.nkp[fp];
-    r.n_kp_cur = P.buf.nkp[fp + 1];
-    r.n_matches = P.buf.nmatch[p];
+    r.n_kp_prev = h.nkp_prev;
+    r.n_kp_cur = h.nkp_cur;
+    r.n_matches = g.m_arr[p];
     r.n_inliers = info[1];
     r.n_good = ok ? g.good[p] : 0;
     r.ransac_iters = info[2];
     // ECAP (a buffer overflowed) > ENOFEAT (an empty frame: the reference's
     // bf.match(None, ...) raises, v3:219) > the RANSAC / pose status.
-    r.status = (P.buf.status[fp] | P.buf.status[fp + 1])         ? DVO_ECAP
-               : (P.buf.nkp[fp] == 0 || P.buf.nkp[fp + 1] == 0) ? DVO_ENOFEAT
-                                                              : info[3];
+    r.status = h.flags ? DVO_ECAP : (h.nkp_prev == 0 || h.nkp_cur == 0) ? DVO_ENOFEAT : info[3];
     r.n_models = info[0] / 3;
     r.n_hypotheses = g.rs[p].h1;  // hypotheses [0, h1) were sampled and solved
     r.pad0 = 0;
@@ -2373,6 +2474,7 @@ hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_re
                            hipEvent_t* ev, bool one_round) {
     const int pairs = stream_pairs(P);
     if (pairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_header_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, P, P.buf.hdr);
     mark(ev, 6, 0, s);
     hipError_t e = launch_geometry_args(g, pairs, kStageNormalize | kStageRansac | (one_round ? kStageOneRound : 0), s);
     mark(ev, 6, 1, s);
@@ -2380,8 +2482,26 @@ hipError_t launch_geometry(const StreamParams& P, const GeomArgs& g, dvo_pair_re
     mark(ev, 7, 0, s);
     e = launch_geometry_args(g, pairs, kStagePose, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(records_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, P, g, records);
+    hipLaunchKernelGGL(records_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g, P.buf.hdr, pairs, records);
     mark(ev, 7, 1, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_header(const StreamParams& P, PairHeader* hdr, hipStream_t s) {
+    const int pairs = stream_pairs(P);
+    if (pairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_header_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, P, hdr);
+    return hipGetLastError();
+}
+
+// A set whose last round has run: E and info (findEssentialMat's result), recoverPose, the records.
+hipError_t launch_retire(const GeomArgs& g_set, int pairs, const PairHeader* hdr, dvo_pair_record* records,
+                         hipStream_t s) {
+    if (pairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ransac_finish_kernel, dim3(pairs), dim3(256), 0, s, g_set);
+    hipError_t e = launch_geometry_args(g_set, pairs, kStagePose, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(records_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, g_set, hdr, pairs, records);
     return hipGetLastError();
 }
 
@@ -2426,7 +2546,13 @@ hipError_t launch_pose_chain(const double* T_rel, int n, double* T_carry, double
 // Test hooks: the sampler / replay kernels on one pair whose RansacState the
 // caller set (api.cpp dvo_test_ransac_*).
 hipError_t launch_test_ransac_sample(const GeomArgs& g, hipStream_t s) {
-    hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, s, g, 1, 1, 1 << 30);
+    RoundSpec sp{};  // one pair continuing (round 1) from the caller's state, no bound
+    sp.nsets = 1;
+    sp.F = 1;
+    sp.round[0] = 1;
+    sp.npairs[0] = 1;
+    sp.bound[0] = sp.bound[1] = 1 << 30;
+    hipLaunchKernelGGL(ransac_sample_kernel, dim3(1), dim3(64), 0, s, g, sp);
     return hipGetLastError();
 }
 hipError_t launch_test_ransac_replay(const GeomArgs& g, hipStream_t s) {

@@ -52,6 +52,7 @@ class FrameStream:
         # frames), so they stay referenced until the next process() or close(), whatever the
         # caller keeps and whether or not sync() has drained _held.
         self._last = ()
+        self._pending = {}  # records of submitted, not yet retired batches (by device address)
         self.width, self.height, self.max_frames, self.nfeatures = width, height, max_frames, nfeatures
         self.K = K.reshape(3, 3)
 
@@ -79,6 +80,8 @@ class FrameStream:
             wait_torch = True  # the zero-fill runs on torch's stream: order the library's writes after it
         if wait_torch:
             self._after_torch()
+        if n > 1:
+            self._pending[records.data_ptr()] = records
         if undistort is not None:  # ops.Undistorter: frames are remapped into the stream's slab first
             self.ctx.check(self.ctx.lib.dvo_stream_process_undistorted(
                 self.h, undistort.h_, frames.data_ptr(), n, frames.stride(0), frames.stride(1),
@@ -86,6 +89,7 @@ class FrameStream:
         else:
             self.ctx.check(self.ctx.lib.dvo_stream_process(self.h, frames.data_ptr(), n, frames.stride(0),
                                                            frames.stride(1), records.data_ptr() if n > 1 else None))
+        self._take_retired()  # this batch, and any submitted before it (drained)
         self._last = (frames, records)
         self._hold(frames, records)
         return records
@@ -110,11 +114,99 @@ class FrameStream:
             wait_torch = True
         if wait_torch:
             self._after_torch()
+        self._pending[records.data_ptr()] = records
         self.ctx.check(self.ctx.lib.dvo_stream_process_pairs(self.h, frames.data_ptr(), n2 // 2, frames.stride(0),
                                                              frames.stride(1), records.data_ptr()))
+        self._take_retired()
         self._last = (frames, records)
         self._hold(frames, records)
         return records
+
+    # ---- pipelined batches (dvo_stream_submit): see include/dvo.h ------------------------------
+    @staticmethod
+    def pipeline_depth() -> int:
+        from ._native import load_library
+        return int(load_library().dvo_pipeline_depth())
+
+    def _check_frames(self, frames, pairs_layout=False):
+        if frames.dtype != torch.uint8 or frames.dim() != 3 or not frames.is_cuda:
+            raise ValueError("frames must be a uint8 [n, H, W] device tensor")
+        n, h, w = frames.shape
+        if (h, w) != (self.height, self.width):
+            raise ValueError(f"frame size {w}x{h} != stream {self.width}x{self.height}")
+        if frames.stride(2) != 1 or frames.stride(1) < w:
+            raise ValueError("frames rows must be contiguous")
+        if pairs_layout and (n % 2 or n == 0):
+            raise ValueError("frames must hold an even, non-zero number of frames (pairs 2p, 2p+1)")
+        return n
+
+    def submit(self, frames: torch.Tensor, records: torch.Tensor, wait_torch: bool = True) -> list:
+        """Pipelined batch (dvo_stream_submit): detection and matching of these
+        frames, then one merged RANSAC round of the pending batches.  `records`
+        (n - 1 records) is complete once the batch retires, pipeline_depth() - 1
+        submits later or at drain(); it is kept referenced until then.  Returns
+        the batches this call retired, oldest first, as (records, pairs)."""
+        n = self._check_frames(frames)
+        if n < 2:
+            raise ValueError("a submitted batch needs >= 2 frames")
+        if records.numel() < (n - 1) * PAIR_RECORD_DTYPE.itemsize:
+            raise ValueError("records too small")
+        if wait_torch:
+            self._after_torch()
+        self.ctx.check(self.ctx.lib.dvo_stream_submit(self.h, frames.data_ptr(), n, frames.stride(0),
+                                                      frames.stride(1), records.data_ptr()))
+        self._pending[records.data_ptr()] = records
+        self._hold(frames, records)
+        return self._take_retired()
+
+    def submit_pairs(self, frames: torch.Tensor, records: torch.Tensor, wait_torch: bool = True) -> list:
+        """submit() with the reference's schedule (pair p = frames 2p, 2p+1; process_pairs)."""
+        n2 = self._check_frames(frames, pairs_layout=True)
+        if records.numel() < (n2 // 2) * PAIR_RECORD_DTYPE.itemsize:
+            raise ValueError("records too small")
+        if wait_torch:
+            self._after_torch()
+        self.ctx.check(self.ctx.lib.dvo_stream_submit_pairs(self.h, frames.data_ptr(), n2 // 2, frames.stride(0),
+                                                            frames.stride(1), records.data_ptr()))
+        self._pending[records.data_ptr()] = records
+        self._hold(frames, records)
+        return self._take_retired()
+
+    def drain(self) -> list:
+        """Run the pending batches' remaining rounds and retire them (oldest first)."""
+        self.ctx.check(self.ctx.lib.dvo_stream_drain(self.h))
+        return self._take_retired()
+
+    def _take_retired(self) -> list:
+        from ._native import _vp
+        cap = 16
+        recs = (_vp * cap)()
+        pairs = (ctypes.c_int * cap)()
+        n = self.ctx.lib.dvo_stream_retired(self.h, recs, pairs, cap)
+        out = []
+        for i in range(min(n, cap)):
+            t = self._pending.pop(recs[i], None)
+            if t is None:
+                raise RuntimeError("retired records that were not submitted through this FrameStream")
+            out.append((t, int(pairs[i])))
+        return out
+
+    def pose_tail_batch(self, records: torch.Tensor, pairs: int, corners_prev: torch.Tensor,
+                        corners_cur: torch.Tensor, marker_length: float, T_rel: torch.Tensor,
+                        T_abs: torch.Tensor, wait_torch: bool = False):
+        """Device pose tail over a retired batch's records (dvo_stream_pose_tail_batch), on this
+        stream's carry (shared with share_pose)."""
+        k = corners_prev.shape[1]
+        if corners_prev.shape[0] < pairs or corners_cur.shape[0] < pairs or T_rel.shape[0] < pairs \
+                or T_abs.shape[0] < pairs:
+            raise ValueError("corners / outputs hold fewer pairs than the batch")
+        if wait_torch:
+            self._after_torch()
+        self.ctx.check(self.ctx.lib.dvo_stream_pose_tail_batch(
+            self.h, records.data_ptr(), int(pairs), corners_prev.data_ptr(), corners_cur.data_ptr(), k,
+            float(marker_length), T_rel.data_ptr(), T_abs.data_ptr()))
+        self._hold(records, corners_prev, corners_cur, T_rel, T_abs)
+        return T_rel, T_abs
 
     def _hold(self, *tensors):
         """Keep the tensors the library's stream reads or writes alive until that
@@ -227,6 +319,7 @@ class FrameStream:
             if getattr(self, "_held", None):
                 self._held.clear()
             self._last = ()
+            self._pending = {}
 
     def __del__(self):
         try:

@@ -230,6 +230,27 @@ int dvo_stream_sync(dvo_stream* s);
  * timing leg of bench.py. */
 int dvo_stream_process_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
                              dvo_pair_record* d_records);
+/* Pipelined batches.  findEssentialMat's RANSAC loop (RANSACPointSetRegistrator::run,
+ * the hot part of v3:297) runs in rounds of hypotheses, [0, 32), [32, 64), [64, 128),
+ * [128, 256), then the rest up to the adaptive bound, each round stopping where the
+ * sequential loop would (the result is the loop's, bit for bit, whatever the rounds).
+ * dvo_stream_process runs a batch's rounds back to back.  dvo_stream_submit runs
+ * detection and matching of its batch and then ONE merged round in which each of the
+ * last dvo_pipeline_depth() submitted batches takes its next round; the batch whose last
+ * round ran is retired (recoverPose, its records written), so a batch's records are
+ * complete dvo_pipeline_depth() - 1 submits later, or after dvo_stream_drain.  The
+ * records buffer and frames of every pending batch must stay allocated until then
+ * (frames only until the submit's detection has run).  dvo_stream_retired lists the
+ * batches the last submit / drain / process call retired, oldest first (their records
+ * pointers and pair counts), returning how many; dvo_stream_pose_tail_batch runs the
+ * pose tail over one of them.  Records are identical to dvo_stream_process's. */
+int dvo_pipeline_depth(void);
+int dvo_stream_submit(dvo_stream* s, const uint8_t* d_frames, int n_frames, int64_t frame_stride, int stride,
+                      dvo_pair_record* d_records);
+int dvo_stream_submit_pairs(dvo_stream* s, const uint8_t* d_frames, int n_pairs, int64_t frame_stride, int stride,
+                            dvo_pair_record* d_records);
+int dvo_stream_drain(dvo_stream* s);
+int dvo_stream_retired(dvo_stream* s, void** records, int* pairs, int cap);
 /* One pair of HOST frames through the whole per-pair path in one synchronous
  * call: the device half of visual_odometry_calculations (v3:384-408) up to
  * recoverPose (v3:303) -- detectAndCompute of both frames (v3:387-392),
@@ -274,6 +295,10 @@ int dvo_stream_reset_pose(dvo_stream* s, const double* P0 /* host 12 */, const d
 int dvo_stream_share_pose(dvo_stream* s, dvo_stream* owner);
 int dvo_stream_pose_tail(dvo_stream* s, const double* d_corners_prev, const double* d_corners_cur, int k,
                          double marker_length, double* d_T_rel, double* d_T_abs);
+/* The same for a retired batch's records (pipelined submits; pairs = its pair count). */
+int dvo_stream_pose_tail_batch(dvo_stream* s, const dvo_pair_record* d_records, int pairs, const double* d_corners_prev,
+                               const double* d_corners_cur, int k, double marker_length, double* d_T_rel,
+                               double* d_T_abs);
 
 /* The same pose tail over caller-supplied pair records: the reassembly step of
  * one pose stream sharded across ranks.  Every rank computes
