@@ -781,16 +781,17 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
 
     def step(i):
         j = i % n_windows
-        return run.step(pools[j], corners[j][:-1], corners[j][1:], wait_torch=False)[0]  # frames resident
+        run.step(pools[j], corners[j][:-1], corners[j][1:], wait_torch=False)  # frames resident
 
     sync_all = run.sync
-    for i in range(args.warmup):
+    prime = max(args.warmup, run.prime_steps)  # the pipeline is full: every timed step retires one window
+    for i in range(prime):
         step(i)
     sync_all()
     if not args.no_profile:
         for f in run.fss:
             f.set_profiling(True)
-    per_run = timed_runs(args, step, sync_all, args.warmup, dist=dist,
+    per_run = timed_runs(args, step, sync_all, prime, dist=dist,
                          device=torch.device("cpu") if run.host_gather else dev)
     value, runs = runs_summary(per_run, WP * args.steps)
     elapsed = WP * args.steps / value
@@ -802,8 +803,10 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
             for kk, v in sm.items():
                 stage_ms[kk] = stage_ms.get(kk, 0.0) + v
             f.set_profiling(False)
+    run.drain()
     # window 0 once more, every rank: its gathered records are what rank 0 checks against the oracle
-    recs = run.step(pools[0], corners[0][:-1], corners[0][1:], wait_torch=False)[0]
+    outs = run.step(pools[0], corners[0][:-1], corners[0][1:], wait_torch=False) + run.drain()
+    recs = outs[-1][0]
     sync_all()
     recs = recs.cpu().numpy().view(PAIR_RECORD_DTYPE).copy()
     if rank == 0:
@@ -841,6 +844,7 @@ def main_sharded(args, world, rank, local_rank, backend, dev, scene):
                                       + ("gloo all_gather (rehearsal)" if run.host_gather else "RCCL all_gather")
                                       + " of records and marker corners, rank-0 device pose tail and chain",
                        "streams_in_flight": S, "rccl_world": dist.get_world_size(),
+                       "ransac_pipeline": {"depth": run.D, "prime_steps": prime},
                        "backend": "gloo" if run.host_gather else "nccl (RCCL)",
                        "pairs_per_rank": run.n_local, "window_pairs": WP,
                        "pairs_ok": f"{int(np.sum(recs['status'] == 0))}/{len(recs)}", "mean_matches": round(m_avg, 1),

@@ -140,16 +140,24 @@ class ShardedPoseStream:
 
 class ShardedStreamRunner:
     """One rank's loop over a sharded pose stream (bench.py main_sharded and
-    tests/test_gpu_sharded.py run this same code): `streams` windows in flight,
-    each on its own FrameStream / HIP stream and its own ShardedPoseStream
-    send buffer, and on rank 0 one PoseTail whose carry continues across
+    tests/test_gpu_sharded.py run this same code): `streams` library streams,
+    window w on stream w mod streams, each window's batch submitted pipelined
+    (FrameStream.submit: its RANSAC rounds run merged with the stream's next
+    pipeline_depth() - 1 windows'), so a window's records are complete -- and
+    exchanged -- when it retires.  Every (stream, in-flight slot) has its own
+    ShardedPoseStream send buffer; the library writes the window's records
+    straight into it.  Rank 0 keeps one PoseTail whose carry continues across
     windows.
 
-    `step(frames, c_prev, c_cur)` enqueues one window: frames = the rank's
+    `step(frames, c_prev, c_cur)` submits one window: frames = the rank's
     n_local + 1 device frames, c_prev / c_cur its n_local pairs' corners.
-    Returns (records, T_rel, T_abs): the window's gathered records (every
-    rank) and rank 0's relative / absolute poses (None elsewhere), valid until
-    the same slot is reused `streams` steps later.
+    Returns the windows retired by this step, oldest first (one per step once
+    prime_steps windows are in flight), each as (records, T_rel, T_abs): the
+    window's gathered records (every rank) and rank 0's relative / absolute
+    poses (None elsewhere), valid until the window's send slot retires again
+    (streams x pipeline_depth() steps later).
+    `drain()` retires the windows still in flight the same way.  Every rank
+    calls step / drain in the same order, so the collectives line up.
 
     Ordering without host syncs on the device-gather path: the library stream
     waits for the slot's previous collective before writing its records;
@@ -159,47 +167,68 @@ class ShardedStreamRunner:
     def __init__(self, width: int, height: int, K, nfeatures: int, window_pairs: int, world: int, rank: int,
                  marker_length: float, ctx=None, device=None, max_iters: int = 1000, streams: int = 2, k: int = 4,
                  host_gather: bool = False, group=None):
+        import collections
         import torch
         from droplet_visual_odometry_amd._native import Context
         from droplet_visual_odometry_amd.stream import FrameStream, PoseTail
         self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
         dev = torch.device("cuda", self.ctx.device)
         self.S, self.rank, self.host_gather = max(1, streams), rank, host_gather
-        self.shs = [ShardedPoseStream(world, rank, window_pairs, dev, k=k, group=group, host_gather=host_gather)
-                    for _ in range(self.S)]
-        self.n_local = self.shs[0].n_local
+        self.D = FrameStream.pipeline_depth()
+        self.shs = [[ShardedPoseStream(world, rank, window_pairs, dev, k=k, group=group, host_gather=host_gather)
+                     for _ in range(self.D)] for _ in range(self.S)]
+        self.n_local = self.shs[0][0].n_local
         self.fss = [FrameStream(width, height, K, nfeatures=nfeatures, max_frames=self.n_local + 1,
                                 max_iters=max_iters, ctx=self.ctx) for _ in range(self.S)]
         self.tail = PoseTail(K, marker_length, ctx=self.ctx) if rank == 0 else None
-        self.T_rel = [torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev) for _ in range(self.S)] \
-            if rank == 0 else None
-        self.T_abs = [torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev) for _ in range(self.S)] \
-            if rank == 0 else None
+        if rank == 0:  # rank 0's poses of each slot's window
+            for row in self.shs:
+                for sh in row:
+                    sh.T_rel = torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev)
+                    sh.T_abs = torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev)
+        self.fifo = [collections.deque() for _ in range(self.S)]  # (send slot, global window number) in flight
+        self.nsub = [0] * self.S
         self.i = 0
+        self.prime_steps = self.S * (self.D - 1)
 
     def step(self, frames, c_prev, c_cur, wait_torch: bool = True):
         """wait_torch (default): order the library stream after work queued on
         torch's current stream -- the frames' producer and, on a slot's first
         use, the zero-fill of its send buffer.  Pass False only for frames that
-        are already resident (the slot's first use is still ordered)."""
-        import torch
+        are already resident (a slot's first use is still ordered)."""
         k = self.i % self.S
-        first_use = self.i < self.S
-        self.i += 1
-        fs, sh = self.fss[k], self.shs[k]
+        fs = self.fss[k]
+        sh = self.shs[k][self.nsub[k] % self.D]
+        first_use = self.nsub[k] < self.D
+        self.nsub[k] += 1
         if frames.shape[0] != self.n_local + 1:
             raise ValueError(f"rank {self.rank} needs {self.n_local + 1} frames per window")
         fs.wait_event(sh.done)  # the slot's previous collective has read its send buffer
-        fs.process(frames, sh.records, wait_torch=wait_torch or first_use)
+        sh.set_corners(c_prev, c_cur)  # torch's stream, after that collective
+        self.fifo[k].append((sh, self.i))
+        self.i += 1
+        retired = fs.submit(frames, sh.records, wait_torch=wait_torch or first_use)
+        return [self._exchange(k, self.fifo[k].popleft()[0]) for _ in retired]
+
+    def drain(self):
+        done = []
+        for k, fs in enumerate(self.fss):
+            for _ in fs.drain():
+                sh, g = self.fifo[k].popleft()
+                done.append((g, k, sh))
+        return [self._exchange(k, sh) for _, k, sh in sorted(done, key=lambda t: t[0])]
+
+    def _exchange(self, k, sh):
+        import torch
+        fs = self.fss[k]
         if self.host_gather:
             fs.sync()
         else:
             torch.cuda.current_stream(fs.device).wait_event(fs.record_event())
-        sh.set_corners(c_prev, c_cur)
         recs, cp, cc = sh.exchange()
         if self.tail is None:
             return recs, None, None
-        T_rel, T_abs = self.tail.run(recs, cp, cc, self.T_rel[k], self.T_abs[k])
+        T_rel, T_abs = self.tail.run(recs, cp, cc, sh.T_rel, sh.T_abs)
         return recs, T_rel, T_abs
 
     def sync(self):

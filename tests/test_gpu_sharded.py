@@ -67,13 +67,18 @@ def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, strea
                                     streams=streams, host_gather=backend == "gloo")
     got_rec, got_Trel, got_Tabs = [], [], []
     pending = []
-    for w in range(windows):
-        p0, p1, f0, f1 = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
-        recs, T_rel, T_abs = run.step(d_frames[f0:f1], d_corners[f0:f1 - 1], d_corners[f0 + 1:f1])
+
+    def keep(outs):
         # device copies on torch's stream (ordered after the collective / the tail), read back
         # only at the end: no host sync between windows, so slots are reused while in flight
-        pending.append((recs.clone(), T_rel.clone() if T_rel is not None else None,
-                        T_abs.clone() if T_abs is not None else None))
+        for recs, T_rel, T_abs in outs:
+            pending.append((recs.clone(), T_rel.clone() if T_rel is not None else None,
+                            T_abs.clone() if T_abs is not None else None))
+
+    for w in range(windows):
+        p0, p1, f0, f1 = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
+        keep(run.step(d_frames[f0:f1], d_corners[f0:f1 - 1], d_corners[f0 + 1:f1]))
+    keep(run.drain())
     run.sync()
     for recs, T_rel, T_abs in pending:
         got_rec.append(recs.cpu().numpy())
@@ -137,14 +142,14 @@ def test_sharded_stream_equals_single_rank(gpu_ctx, W, H, NF, n_pairs, windows, 
 @pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])
 def test_sharded_rccl_path_two_slots_in_flight(gpu_ctx, W, H, NF):
     """The RCCL branch of the sharded loop (device all-gather, no host syncs):
-    world size 1 on the box's one GPU, two send-buffer slots in flight over six
-    windows, so every slot is rewritten while the previous windows' collectives
-    and pose tails are still queued.  Any missing stream order (records read
+    world size 1 on the box's one GPU, two streams with pipeline_depth()
+    send-buffer slots each over fourteen windows, so every slot is rewritten
+    while the previous windows' collectives and pose tails are still queued.  Any missing stream order (records read
     before written, a send buffer rewritten before its collective read it, the
     tail racing the gather) shows as a mismatch with the single-rank stream.
     Also at BASELINE configs[3]'s 1280x720 / 2000 features."""
     import torch.multiprocessing as mp
-    n_pairs, windows, blank = 8, 6, (12,)
+    n_pairs, windows, blank = 8, 14, (12,)  # more windows than streams x pipeline depth: slots reused
     F = n_pairs * windows + 1
     mgr = mp.Manager()
     out = mgr.dict()
