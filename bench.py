@@ -35,6 +35,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); streams that
+# share a queue run in order, so the copy stream of the host-fed leg queued behind a library stream's
+# kernels (host-fed 45.0 K -> 58.1 K frames/s with 8; the device-resident run is unchanged,
+# profiles/r05h_queues.txt).  The bench runs two library streams, torch's stream, a side stream and a
+# copy stream: 8 queues give each its own.  Set before the HIP runtime starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
@@ -585,16 +591,22 @@ def host_fed_leg(args, pool, pipe, n_windows, stream_value):
     slots = [torch.empty((B + 1,) + tuple(pool.shape[1:]), dtype=pool.dtype, device=pool.device) for _ in range(R)]
     cs = torch.cuda.Stream(device=pool.device)
     used = [None] * R
+    cev = []  # (start, end) timing events of the timed copies
     torch.cuda.synchronize()
 
-    def step(i):
+    def step(i, timed=False):
         s0, k, r = (i % n_windows) * B, i % S, i % R
         with torch.cuda.stream(cs):
             if used[r] is not None:
                 cs.wait_event(used[r])  # the detection that last read this slot has finished
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(cs)
             slots[r].copy_(hpool[s0:s0 + B + 1], non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=timed)
             ev.record(cs)
+            if timed:
+                cev.append((e0, ev))
         fs = pipe.fss[k]
         fs.wait_event(ev)
         pipe.step(k, slots[r], s0)
@@ -606,9 +618,10 @@ def host_fed_leg(args, pool, pipe, n_windows, stream_value):
     pipe.sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(prime + i)
+        step(prime + i, timed=True)
     pipe.sync()
     dt = time.perf_counter() - t0
+    copy_ms = float(np.mean([a.elapsed_time(b) for a, b in cev])) if cev else None
     pipe.drain()
     pipe.sync()
     # the link alone: the same copies back to back on the copy stream
@@ -630,6 +643,8 @@ def host_fed_leg(args, pool, pipe, n_windows, stream_value):
             "h2d_bytes_per_step": nb, "h2d_link_GBps": round(link, 2),
             "link_bound_frames_per_s": round(link * 1e9 / (nb / (B + 1)) * B / (B + 1), 1),
             "vs_device_resident": round(value / stream_value, 4),
+            "copy_ms_during_compute": round(copy_ms, 3) if copy_ms else None,
+            "copy_ms_alone": round(1e3 * dl / reps, 3),
             "schedule": "pinned host frames, async H2D on a copy stream into a ring of S+2 device slots overlapped "
                         "with compute; B+1 frames copied per B-pair step"}
 
@@ -645,7 +660,7 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
     process.py:172-252 is the single stream being reassembled)."""
     import torch
     from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
-    from droplet_visual_odometry_amd.stream import PoseTail
+    from droplet_visual_odometry_amd.stream import HostPoseChain, PoseTail
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     B, S, N = args.batch, len(pipe.fss), args.tail_world
     dev = pool.device
@@ -654,6 +669,7 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
     cp = corners[:B].repeat(N, 1, 1).contiguous()
     cc = corners[1:B + 1].repeat(N, 1, 1).contiguous()
     tail = PoseTail(K, MARKER_LEN, ctx=ctx)
+    hchain = HostPoseChain(N * B, 2 * S + 1, dev)
     T_rel = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     T_abs = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     cur = torch.cuda.current_stream(dev)
@@ -669,7 +685,11 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
         ev = torch.cuda.Event()
         ev.record(cur)
         done[k] = ev
-        tail.run(wrecs[k], cp, cc, T_rel[k], T_abs[k])
+        # rank 0's half of the split tail (dist.ShardedStreamRunner): T_rel of its own B pairs, then
+        # (after the T_rel all-gather, stood in for by the window's T_rel buffer) the serial chain on
+        # a host thread
+        tail.rel_range(wrecs[k], cp, cc, 0, pairs, T_rel[k])
+        hchain.submit(T_rel[k])
 
     def run(with_tail):
         pipe.on_retire = on_retire if with_tail else (lambda *a: None)
@@ -687,27 +707,42 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
         for i in range(args.steps):
             step(prime + i)
         pipe.sync()
+        hchain.wait()  # every window chained
         dt = 1e3 * (time.perf_counter() - t0) / args.steps
         pipe.drain()
         pipe.sync()
+        hchain.wait()
         return dt
 
     base = run(False)
     with_tail = run(True)
     pipe.on_retire = None
-    # the tail's own duration on an otherwise idle GPU (one launch of pose_tail + pose_chain over N x B records)
+    # rank 0's tail alone: its pairs' T_rel on the idle GPU, the host chain over N x B
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cur)
+    tail.rel_range(wrecs[0], cp, cc, 0, B, T_rel[0])
+    e1.record(cur)
+    torch.cuda.synchronize()
+    rel_alone = e0.elapsed_time(e1)
+    th = time.perf_counter()
+    hchain.submit(T_rel[0]).result()
+    host_chain_ms = 1e3 * (time.perf_counter() - th)
+    hchain.close()
+    # the unsplit tail (every pair's T_rel on rank 0, round 4's schedule), for comparison
     e0.record(cur)
     tail.run(wrecs[0], cp, cc, T_rel[0], T_abs[0])
     e1.record(cur)
     torch.cuda.synchronize()
-    alone = e0.elapsed_time(e1)
+    alone_unsplit = e0.elapsed_time(e1)
     return {"world": N, "pairs_per_window": N * B, "ms_per_step_without_tail": round(base, 3),
             "ms_per_step_with_tail": round(with_tail, 3), "added_ms_per_step": round(with_tail - base, 3),
-            "added_frac": round((with_tail - base) / base, 4), "tail_alone_ms": round(alone, 3),
-            "note": "rank 0's pose tail + serial absolute chain over a world-N window (N x B gathered records) on "
-                    "torch's stream beside the library streams; steps of B new pairs per rank (weak scaling)"}
+            "added_frac": round((with_tail - base) / base, 4), "rel_range_alone_ms": round(rel_alone, 3),
+            "host_chain_ms": round(host_chain_ms, 3), "unsplit_device_tail_alone_ms": round(alone_unsplit, 3),
+            "note": "rank 0's share of the split pose tail (dist.ShardedStreamRunner): T_rel of its own B pairs on "
+                    "torch's stream beside the library streams, then the serial absolute chain over the world-N "
+                    "window (N x B gathered T_rel) on a host thread (dvo_pose_chain_host); steps of B new pairs "
+                    "per rank (weak scaling)"}
 
 
 def pose_check_opencv32(pool, K, nfeatures, max_iters, n_pairs, ctx):

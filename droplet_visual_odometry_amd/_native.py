@@ -133,6 +133,8 @@ _SIGNATURES = {
     "dvo_stream_pose_tail": ([_vp, _vp, _vp, _c, _d, _vp, _vp], _c),
     "dvo_pose_tail_records": ([_vp, _vp, _c, _vp, _vp, _vp, _c, _d, _vp, _vp, _vp, _vp], _c),
     "dvo_pose_chain": ([_vp, _vp, _c, _vp, _vp, _vp], _c),
+    "dvo_pose_chain_host": ([_vp, _c, _vp, _vp], _c),
+    "dvo_pose_rel_range": ([_vp, _vp, _c, _c, _c, _vp, _vp, _vp, _c, _d, _vp, _vp, _vp], _c),
     "dvo_stream_stage_times": ([_vp, _vp, _ip], _c),
     "dvo_stream_get_features": ([_vp, _c, _vp, _vp, _c, _ip], _c),
     "dvo_stream_get_matches": ([_vp, _c, _vp, _c, _ip], _c),

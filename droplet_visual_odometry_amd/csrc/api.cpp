@@ -850,6 +850,44 @@ int dvo_pose_tail_records(dvo_ctx* ctx, const dvo_pair_record* d_records, int pa
     return DVO_OK;
 }
 
+int dvo_pose_rel_range(dvo_ctx* ctx, const dvo_pair_record* d_records, int pairs, int p0, int n, const double* K,
+                       const double* d_corners_prev, const double* d_corners_cur, int k, double marker_length,
+                       double* d_P_carry, double* d_T_rel, void* hip_stream) {
+    if (!ctx) return DVO_EINVAL;
+    if (pairs < 0 || p0 < 0 || n < 0 || p0 + n > pairs || !K)
+        return fail(ctx, DVO_EINVAL, "pose range needs 0 <= p0 <= p0 + n <= pairs and K");
+    if (pairs == 0) return DVO_OK;
+    if (!d_records || !d_P_carry || (n > 0 && (k < 2 || !d_corners_prev || !d_corners_cur || !d_T_rel)))
+        return fail(ctx, DVO_EINVAL, "pose range needs records, the P carry, >= 2 corners per frame and T_rel");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(launch_pose_rel_range(d_records, pairs, p0, n, K, d_corners_prev, d_corners_cur, k, marker_length,
+                                  d_P_carry, d_T_rel, hip_stream ? (hipStream_t)hip_stream : ctx->stream));
+    return DVO_OK;
+}
+
+// The chain on the host, in the device kernel's arithmetic order (pose_chain_kernel: element
+// (r, c) = ((t_r0 A_0c + t_r1 A_1c) + t_r2 A_2c) + t_r3 A_3c; this file is built with
+// -ffp-contract=off, so each product and sum rounds as written).
+int dvo_pose_chain_host(const double* T_rel, int n, double* T_carry, double* T_abs) {
+    if (n < 0 || (n > 0 && (!T_rel || !T_carry || !T_abs))) return DVO_EINVAL;
+    double t[16];
+    std::memcpy(t, T_carry, sizeof(t));
+    for (int p = 0; p < n; ++p) {
+        const double* A = T_rel + (size_t)p * 16;
+        double u[16];
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) {
+                const double m0 = t[r * 4 + 0] * A[0 * 4 + c], m1 = t[r * 4 + 1] * A[1 * 4 + c];
+                const double m2 = t[r * 4 + 2] * A[2 * 4 + c], m3 = t[r * 4 + 3] * A[3 * 4 + c];
+                u[r * 4 + c] = ((m0 + m1) + m2) + m3;
+            }
+        std::memcpy(t, u, sizeof(t));
+        std::memcpy(T_abs + (size_t)p * 16, t, sizeof(t));
+    }
+    std::memcpy(T_carry, t, sizeof(t));
+    return DVO_OK;
+}
+
 int dvo_pose_chain(dvo_ctx* ctx, const double* d_T_rel, int n, double* d_T_carry, double* d_T_abs, void* hip_stream) {
     if (!ctx) return DVO_EINVAL;
     if (n < 0 || (n > 0 && (!d_T_rel || !d_T_carry || !d_T_abs)))

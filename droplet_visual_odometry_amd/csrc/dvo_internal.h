@@ -364,6 +364,11 @@ hipError_t launch_pose_tail(const dvo_pair_record* rec, int pairs, const double*
 // its own: the reassembled pose stream of a sharded run); T_carry is updated.
 hipError_t launch_pose_chain(const double* T_rel /*[n][16]*/, int n, double* T_carry /*16*/, double* T_abs,
                              hipStream_t s);
+// The pair-parallel half of the pose tail for pairs [p0, p0 + n) of a window of `pairs` records
+// (T_rel[0 .. n)), then P_carry (12 doubles) advanced past the whole window.
+hipError_t launch_pose_rel_range(const dvo_pair_record* rec, int pairs, int p0, int n, const double* K,
+                                 const double* cprev, const double* ccur, int k, double marker_length, double* P_carry,
+                                 double* T_rel, hipStream_t s);
 hipError_t launch_triangulate(const double* d_P /*24*/, const double* d_x /*4 x k*/, int k, double* d_X, hipStream_t s);
 // Float-descriptor kNN (NORM_L1 / squared L2), dim 64 or 128, k 1..4, over
 // `ranges` = knn_ranges(nq, nt, CU count) train ranges; d_part / d_pidx hold

@@ -2296,6 +2296,7 @@ __device__ void proj_of(const double* K, const double* Rt, double* P) {  // K . 
 struct TailArgs {
     const dvo_pair_record* rec;  // R (9) and t (3) are the record's first 12 doubles: the [R | t] layout
     int pairs;
+    int p0;          // pose_tail_kernel: pairs [p0, pairs) of rec, T_rel[p - p0] (0: the whole window)
     double K[9];
     const double* cprev;
     const double* ccur;
@@ -2315,13 +2316,30 @@ __device__ inline bool rec_ok(const dvo_pair_record* rec, int p) {
 }
 __device__ inline const double* rec_Rt(const dvo_pair_record* rec, int p) { return rec[p].R; }
 
+// P_prev carry after a window of records: the projection of its last successful pair (unchanged
+// when none succeeded), as pose_chain_kernel leaves it.
+__global__ __launch_bounds__(1024) void pose_carry_kernel(TailArgs a) {
+    __shared__ int s_last[16];
+    int last_ok = -1;
+    for (int p = a.pairs - 1 - (int)threadIdx.x; p >= 0 && last_ok < 0; p -= 1024)  // from the end
+        if (rec_ok(a.rec, p)) last_ok = p;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) last_ok = max(last_ok, __shfl_xor(last_ok, o));
+    if ((threadIdx.x & 63) == 0) s_last[threadIdx.x >> 6] = last_ok;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) last_ok = max(last_ok, s_last[w]);
+        if (last_ok >= 0) proj_of(a.K, rec_Rt(a.rec, last_ok), a.carry);
+    }
+}
+
 // The pose tail reads only the 256-B pair records (R, t, status), so a pose
 // stream whose records were computed on several ranks and all-gathered gives
 // the same result as one rank's (dvo_pose_tail_records).
 __global__ void pose_tail_kernel(TailArgs a) {
-    const int p = blockIdx.x * 64 + threadIdx.x;
+    const int p = a.p0 + blockIdx.x * 64 + threadIdx.x;
     if (p >= a.pairs) return;
-    double* Tr = a.T_rel + (int64_t)p * 16;
+    double* Tr = a.T_rel + (int64_t)(p - a.p0) * 16;
     if (!rec_ok(a.rec, p)) {  // the reference would have raised here
         for (int r = 0; r < 16; ++r) Tr[r] = (r % 5 == 0) ? 1.0 : 0.0;
         return;
@@ -2371,6 +2389,9 @@ __global__ void pose_tail_kernel(TailArgs a) {
 // dependency chain of a step is then one quad exchange and 4 dependent f64 ops
 // (round 3 kept a whole row per lane: 28 f64 instructions issued per step).
 // T_rel is staged through LDS 64 pairs at a time and read one step ahead.
+// (Round 5, beside a full batch on the other streams: 1.5 us per step against 80 ns alone with
+// LDS staging, wave priority 3 or registers only (profiles/r05j_*, r05k_*); rank 0 of a sharded
+// run therefore chains on the host, dvo_pose_chain_host.)
 template <int K>
 __device__ __forceinline__ double quad_bcast(double v) {  // lane 4 q + K of the lane's quad
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -2529,6 +2550,26 @@ hipError_t launch_pose_tail(const dvo_pair_record* rec, int pairs, const double*
     a.T_abs = T_abs;
     hipLaunchKernelGGL(pose_tail_kernel, dim3((pairs + 63) / 64), dim3(64), 0, s, a);
     hipLaunchKernelGGL(pose_chain_kernel, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pose_rel_range(const dvo_pair_record* rec, int pairs, int p0, int n, const double* K,
+                                 const double* cprev, const double* ccur, int k, double marker_length, double* P_carry,
+                                 double* T_rel, hipStream_t s) {
+    TailArgs a{};
+    a.rec = rec;
+    a.pairs = p0 + n;
+    a.p0 = p0;
+    for (int i = 0; i < 9; ++i) a.K[i] = K[i];
+    a.cprev = cprev;
+    a.ccur = ccur;
+    a.k = k;
+    a.L = marker_length;
+    a.carry = P_carry;
+    a.T_rel = T_rel;
+    if (n > 0) hipLaunchKernelGGL(pose_tail_kernel, dim3((n + 63) / 64), dim3(64), 0, s, a);
+    a.pairs = pairs;  // the carry leaves the window at its last successful pair
+    hipLaunchKernelGGL(pose_carry_kernel, dim3(1), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

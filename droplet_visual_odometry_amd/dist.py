@@ -98,6 +98,10 @@ class ShardedPoseStream:
         gdev = torch.device("cpu") if host_gather else self.device
         self.recv = torch.empty(world * self.seg, dtype=torch.uint8, device=gdev)
         self.done = None  # torch.cuda.Event recorded after the last collective (device gathers)
+        # the second exchange: T_rel of each rank's own pairs (dvo_pose_rel_range), gathered for rank 0's chain
+        self.p0_local = sum(self.counts[:rank])
+        self.T_send = torch.zeros((self.cap, 4, 4), dtype=torch.float64, device=self.device)
+        self.T_recv = torch.empty((world, self.cap, 4, 4), dtype=torch.float64, device=gdev)
 
     @property
     def records(self):
@@ -137,6 +141,16 @@ class ShardedPoseStream:
             recs, cp, cc = (x.to(self.device) for x in (recs, cp, cc))
         return recs, cp, cc
 
+    def exchange_T(self):
+        """All-gather every rank's T_rel (T_send[:n_local]) and return the window's T_rel in pair
+        order, [window_pairs, 4, 4] on `device`."""
+        import torch
+        import torch.distributed as dist
+        send = self.T_send.cpu() if self.host_gather else self.T_send
+        dist.all_gather_into_tensor(self.T_recv.view(-1), send.view(-1), group=self.group)
+        T = torch.cat([self.T_recv[r, :c] for r, c in enumerate(self.counts)])
+        return T.to(self.device) if self.host_gather else T
+
 
 class ShardedStreamRunner:
     """One rank's loop over a sharded pose stream (bench.py main_sharded and
@@ -153,16 +167,27 @@ class ShardedStreamRunner:
     n_local + 1 device frames, c_prev / c_cur its n_local pairs' corners.
     Returns the windows retired by this step, oldest first (one per step once
     prime_steps windows are in flight), each as (records, T_rel, T_abs): the
-    window's gathered records (every rank) and rank 0's relative / absolute
-    poses (None elsewhere), valid until the window's send slot retires again
-    (streams x pipeline_depth() steps later).
+    window's gathered records (every rank) and rank 0's relative poses (device)
+    and absolute poses (a concurrent.futures.Future of the host [n, 4, 4]
+    array, chained on a host thread; None elsewhere), valid until the window's
+    send slot retires again (streams x pipeline_depth() steps later).
     `drain()` retires the windows still in flight the same way.  Every rank
     calls step / drain in the same order, so the collectives line up.
 
+    The pose tail is split: every rank computes the relative poses of its own
+    pairs from the gathered records (dvo_pose_rel_range: the marker scale
+    triangulates against the last successful pair before it, wherever that
+    was computed), a second all-gather brings the window's T_rel to rank 0,
+    and rank 0 runs only the serial absolute chain, on a host thread
+    (dvo_pose_chain_host: one sequential product per pair, ~50 ns on a CPU
+    core while the GPU runs the next batches); the poses equal one rank's
+    pose tail over the stream bit for bit.
+
     Ordering without host syncs on the device-gather path: the library stream
     waits for the slot's previous collective before writing its records;
-    torch's stream waits for the records before the collective; rank 0's tail
-    runs after the collective on torch's stream (ordered_side_stream)."""
+    torch's stream waits for the records before the collective; the tail
+    halves and the second collective follow on torch's stream
+    (ordered_side_stream)."""
 
     def __init__(self, width: int, height: int, K, nfeatures: int, window_pairs: int, world: int, rank: int,
                  marker_length: float, ctx=None, device=None, max_iters: int = 1000, streams: int = 2, k: int = 4,
@@ -170,7 +195,7 @@ class ShardedStreamRunner:
         import collections
         import torch
         from droplet_visual_odometry_amd._native import Context
-        from droplet_visual_odometry_amd.stream import FrameStream, PoseTail
+        from droplet_visual_odometry_amd.stream import FrameStream, HostPoseChain, PoseTail
         self.ctx = ctx if ctx is not None else Context(0 if device is None else device)
         dev = torch.device("cuda", self.ctx.device)
         self.S, self.rank, self.host_gather = max(1, streams), rank, host_gather
@@ -180,12 +205,9 @@ class ShardedStreamRunner:
         self.n_local = self.shs[0][0].n_local
         self.fss = [FrameStream(width, height, K, nfeatures=nfeatures, max_frames=self.n_local + 1,
                                 max_iters=max_iters, ctx=self.ctx) for _ in range(self.S)]
-        self.tail = PoseTail(K, marker_length, ctx=self.ctx) if rank == 0 else None
-        if rank == 0:  # rank 0's poses of each slot's window
-            for row in self.shs:
-                for sh in row:
-                    sh.T_rel = torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev)
-                    sh.T_abs = torch.empty((window_pairs, 4, 4), dtype=torch.float64, device=dev)
+        # every rank: the P_prev carry and its own pairs' T_rel; rank 0 also the chain, on the host
+        self.tail = PoseTail(K, marker_length, ctx=self.ctx)
+        self.chain = HostPoseChain(window_pairs, self.S * self.D + 1, dev) if rank == 0 else None
         self.fifo = [collections.deque() for _ in range(self.S)]  # (send slot, global window number) in flight
         self.nsub = [0] * self.S
         self.i = 0
@@ -226,20 +248,28 @@ class ShardedStreamRunner:
         else:
             torch.cuda.current_stream(fs.device).wait_event(fs.record_event())
         recs, cp, cc = sh.exchange()
-        if self.tail is None:
+        # the pair-parallel half of the tail on every rank, over its own pairs of the window
+        self.tail.rel_range(recs, cp, cc, sh.p0_local, sh.n_local, sh.T_send)
+        T_rel = sh.exchange_T()
+        if self.rank != 0:
             return recs, None, None
-        T_rel, T_abs = self.tail.run(recs, cp, cc, sh.T_rel, sh.T_abs)
-        return recs, T_rel, T_abs
+        # the serial chain on a host thread (dvo_pose_chain_host): off the GPU, which goes on with the
+        # next windows; T_abs is a Future of the host array
+        return recs, T_rel, self.chain.submit(T_rel)
 
     def sync(self):
         import torch
         for f in self.fss:
             f.sync()
         torch.cuda.synchronize()
+        if self.chain is not None:
+            self.chain.wait()
 
     def close(self):
         for f in self.fss:
             f.close()
+        if self.chain is not None:
+            self.chain.close()
 
 
 def gather_records(records, n_local: int, n_frames: int, group=None):

@@ -378,6 +378,59 @@ class PoseChain:
 
 
 
+class HostPoseChain:
+    """The absolute chain T_abs[p] = T_abs[p-1] . T_rel[p] (v3:367) on a host thread
+    (dvo_pose_chain_host, the device kernel's arithmetic bit for bit): rank 0 of a sharded stream
+    (dist.ShardedStreamRunner).  submit(T_rel) copies the device T_rel into a pinned slot on
+    torch's current stream and returns a Future of the window's T_abs (host, [n, 4, 4] float64);
+    one worker thread chains the windows in submission order, waiting for each copy's event, while
+    the GPU goes on with the next batches.  The carry (16 doubles) continues across windows."""
+
+    def __init__(self, max_pairs: int, slots: int, device, T0=None):
+        import concurrent.futures
+        from ._native import load_library
+        self.lib = load_library()
+        self.device = torch.device(device)
+        self.carry = np.ascontiguousarray(np.eye(4) if T0 is None else np.asarray(T0, np.float64)).reshape(16).copy()
+        self.pinned = [torch.empty((max_pairs, 4, 4), dtype=torch.float64, pin_memory=True) for _ in range(slots)]
+        self.pending = [None] * slots
+        self.n = 0
+        self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+
+    def submit(self, T_rel: torch.Tensor):
+        n = T_rel.shape[0]
+        k = self.n % len(self.pinned)
+        self.n += 1
+        if self.pending[k] is not None:
+            self.pending[k].result()  # the slot's previous chain has read its pinned buffer
+        buf = self.pinned[k]
+        buf[:n].copy_(T_rel, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+
+        def work():
+            ev.synchronize()
+            out = np.empty((n, 4, 4), np.float64)
+            src = buf[:n].numpy()
+            rc = self.lib.dvo_pose_chain_host(src.ctypes.data, n, self.carry.ctypes.data, out.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(f"dvo_pose_chain_host failed ({rc})")
+            return out
+
+        fut = self.pool.submit(work)
+        self.pending[k] = fut
+        return fut
+
+    def wait(self):
+        """Block until every submitted window is chained (raises a chain's error)."""
+        for f in self.pending:
+            if f is not None:
+                f.result()
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
 class PoseTail:
     """Pose tail over pair records (dvo_pose_tail_records): the marker-scaled
     relative poses (v3:309-345) and the absolute chain (v3:367) for records
@@ -431,3 +484,52 @@ class PoseTail:
                 self.ctx.h, records.data_ptr(), n, ptr(self.K), corners_prev.data_ptr(), corners_cur.data_ptr(), k,
                 self.marker_length, self.carry.data_ptr(), T_rel.data_ptr(), T_abs.data_ptr(), st))
         return T_rel, T_abs
+
+    def rel_range(self, records: torch.Tensor, corners_prev: torch.Tensor, corners_cur: torch.Tensor, p0: int,
+                  n: int, T_rel: torch.Tensor) -> torch.Tensor:
+        """The pair-parallel half over pairs [p0, p0 + n) of a gathered window (dvo_pose_rel_range):
+        T_rel[0 .. n), then the P_prev carry advanced past the whole window.  Every rank of a sharded
+        stream runs it over its own pairs; rank 0 chains the gathered T_rel with chain()."""
+        rb = PAIR_RECORD_DTYPE.itemsize
+        pairs = records.numel() // rb
+        k = corners_prev.shape[1]
+        if corners_prev.shape[0] != pairs or corners_cur.shape[0] != pairs:
+            raise ValueError("corners must cover the window's pairs")
+        if T_rel.shape[0] < n or not T_rel.is_contiguous() or T_rel.dtype != torch.float64:
+            raise ValueError("T_rel must be a contiguous float64 [>= n, 4, 4] device tensor")
+        with ordered_side_stream(self.device) as st:
+            self.ctx.check(self.ctx.lib.dvo_pose_rel_range(
+                self.ctx.h, records.data_ptr(), pairs, int(p0), int(n), ptr(self.K), corners_prev.data_ptr(),
+                corners_cur.data_ptr(), k, self.marker_length, self.carry.data_ptr(), T_rel.data_ptr(), st))
+        return T_rel
+
+    def chain(self, T_rel: torch.Tensor, T_abs: torch.Tensor, detached: bool = False) -> torch.Tensor:
+        """The serial absolute chain (dvo_pose_chain) on this tail's T_abs carry.  detached: on the
+        tail's own chain stream, after the work queued on torch's current stream so far, WITHOUT
+        ordering torch's stream after it -- the chain (one wave's dependency chain over the
+        window) then stays off the path of the next collectives; chains still run in call
+        order.  Read T_abs after torch.cuda.synchronize() (or chain_event())."""
+        n = T_rel.shape[0]
+        if not detached:
+            with ordered_side_stream(self.device) as st:
+                self.ctx.check(self.ctx.lib.dvo_pose_chain(self.ctx.h, T_rel.data_ptr(), n,
+                                                           self.carry.data_ptr() + 12 * 8, T_abs.data_ptr(), st))
+            return T_abs
+        if getattr(self, "_chain_stream", None) is None:
+            self._chain_stream = torch.cuda.Stream(self.device)
+        cs = self._chain_stream
+        cs.wait_stream(torch.cuda.current_stream(self.device))
+        self.ctx.check(self.ctx.lib.dvo_pose_chain(self.ctx.h, T_rel.data_ptr(), n, self.carry.data_ptr() + 12 * 8,
+                                                   T_abs.data_ptr(), cs.cuda_stream))
+        T_rel.record_stream(cs)  # torch's allocator keeps T_rel / T_abs until the chain has read / written them
+        T_abs.record_stream(cs)
+        return T_abs
+
+    def chain_event(self):
+        """An event after the detached chains queued so far (None if there were none)."""
+        cs = getattr(self, "_chain_stream", None)
+        if cs is None:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return ev

@@ -317,6 +317,24 @@ int dvo_pose_tail_records(dvo_ctx* ctx, const dvo_pair_record* d_records, int pa
                           const double* d_corners_prev, const double* d_corners_cur, int k, double marker_length,
                           double* d_carry, double* d_T_rel, double* d_T_abs, void* hip_stream);
 
+/* The pair-parallel half of that tail on one rank's run of a gathered window:
+ * T_rel of pairs [p0, p0 + n) of the window's `pairs` records (d_T_rel[0 .. n)),
+ * each triangulating against the last successful pair before it in the window
+ * (or d_P_carry, 12 doubles, when none is), then d_P_carry advanced past the
+ * window (to its last successful pair's K [R | t]).  Every rank runs it over its
+ * own pairs, rank 0 gathers the T_rel and runs dvo_pose_chain: the same values,
+ * bit for bit, as dvo_pose_tail_records over the window on one rank.  Corner
+ * arrays are the window's ([pairs][k][2]).  Asynchronous on hip_stream. */
+int dvo_pose_rel_range(dvo_ctx* ctx, const dvo_pair_record* d_records, int pairs, int p0, int n, const double* K,
+                       const double* d_corners_prev, const double* d_corners_cur, int k, double marker_length,
+                       double* d_P_carry, double* d_T_rel, void* hip_stream);
+
+/* The same chain on the host (host arrays; the device kernel's arithmetic, bit for bit): the
+ * chain is one sequential product per pair, which a CPU core runs in ~50 ns per pair while
+ * the GPU is busy with the next batches, where the one-wave kernel slows to ~1.5 us per pair
+ * (round 5).  Rank 0 of a sharded stream chains the gathered T_rel here. */
+int dvo_pose_chain_host(const double* T_rel, int n, double* T_carry, double* T_abs);
+
 /* The absolute-pose chain of previous_current_matching (v3:367,
  * T_robot_cur = T_robot_prev . T_prev->cur) on its own, for pose streams
  * reassembled from sharded runs: rank 0 all-gathers every

@@ -71,9 +71,8 @@ def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, strea
     def keep(outs):
         # device copies on torch's stream (ordered after the collective / the tail), read back
         # only at the end: no host sync between windows, so slots are reused while in flight
-        for recs, T_rel, T_abs in outs:
-            pending.append((recs.clone(), T_rel.clone() if T_rel is not None else None,
-                            T_abs.clone() if T_abs is not None else None))
+        for recs, T_rel, T_abs in outs:  # T_abs: rank 0's Future of the host-chained poses
+            pending.append((recs.clone(), T_rel.clone() if T_rel is not None else None, T_abs))
 
     for w in range(windows):
         p0, p1, f0, f1 = ddist.shard_window(n_pairs, world, rank, w * n_pairs)
@@ -84,7 +83,7 @@ def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, strea
         got_rec.append(recs.cpu().numpy())
         if T_rel is not None:
             got_Trel.append(T_rel.cpu().numpy())
-            got_Tabs.append(T_abs.cpu().numpy())
+            got_Tabs.append(T_abs.result())
     out[rank] = (np.concatenate(got_rec).tobytes(),
                  np.concatenate(got_Trel).tobytes() if got_Trel else b"",
                  np.concatenate(got_Tabs).tobytes() if got_Tabs else b"")
@@ -118,7 +117,8 @@ def _check(gpu_ctx, out, ranks, W, H, NF, F, blank):
         assert out[r][0] == want_rec, f"rank {r}: gathered records differ from the single-rank stream"
     np.testing.assert_array_equal(np.frombuffer(out[0][1]).reshape(-1, 4, 4), want_Trel)
     got_Tabs = np.frombuffer(out[0][2]).reshape(-1, 4, 4)
-    bad = [i for i in range(len(want_Tabs)) if not np.array_equal(got_Tabs[i], want_Tabs[i])]
+    # bit for bit (the host chain repeats the device chain's arithmetic), signed zeros included
+    bad = [i for i in range(len(want_Tabs)) if got_Tabs[i].tobytes() != want_Tabs[i].tobytes()]
     assert not bad, f"rank 0 T_abs differs at pairs {bad}"
 
 
@@ -177,6 +177,39 @@ def test_pose_chain_equals_pose_tail_chain(gpu_ctx):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(torch.cat([a, b]).cpu().numpy(), T_abs.cpu().numpy())
     np.testing.assert_array_equal(ch.carry.cpu().numpy().reshape(4, 4), T_abs[-1].cpu().numpy())
+    fs.close()
+
+
+def test_host_chain_equals_device_chain(gpu_ctx):
+    """dvo_pose_chain_host (rank 0's chain of a sharded stream) gives the device pose tail's T_abs
+    byte for byte over 600 pairs of real T_rel, in two windows with the carry in between."""
+    import ctypes
+    import torch
+    from conftest import synth_frames
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, marker_corners
+    frames, K = synth_frames(320, 240, range(9))
+    fs = FrameStream(320, 240, K, nfeatures=300, max_frames=9, ctx=gpu_ctx)
+    fs.reset_pose()
+    fs.process(torch.from_numpy(frames).cuda())
+    dc = torch.from_numpy(np.stack([marker_corners(i, K) for i in range(9)])).cuda()
+    T_rel, T_abs = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
+    fs.sync()
+    Tr = np.ascontiguousarray(np.tile(T_rel.cpu().numpy(), (75, 1, 1)))  # 600 pairs
+    dev_abs = torch.empty((600, 4, 4), dtype=torch.float64, device="cuda")
+    carry = torch.from_numpy(np.eye(4).reshape(16).copy()).cuda()
+    gpu_ctx.check(gpu_ctx.lib.dvo_pose_chain(gpu_ctx.h, torch.from_numpy(Tr).cuda().data_ptr(), 600,
+                                             carry.data_ptr(), dev_abs.data_ptr(), None))
+    torch.cuda.synchronize()
+    hc = np.eye(4).reshape(16).copy()
+    out = np.empty((600, 4, 4))
+    for a, b in ((0, 250), (250, 600)):
+        part = np.ascontiguousarray(Tr[a:b])
+        o = np.empty_like(part)
+        assert gpu_ctx.lib.dvo_pose_chain_host(part.ctypes.data, b - a, hc.ctypes.data, o.ctypes.data) == 0
+        out[a:b] = o
+    assert out.tobytes() == dev_abs.cpu().numpy().tobytes()
+    assert hc.tobytes() == carry.cpu().numpy().tobytes()
     fs.close()
 
 
