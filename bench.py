@@ -963,10 +963,10 @@ def chained_ate(fs, pool, corners, K, ref, B):
 
 
 def pmc_doc(pattern, W, H, N):
-    """(path, document) of the newest committed PMC document under profiles/
-    (round tags sort by name) collected on this workload, or None."""
+    """(path, document) of the committed PMC document under profiles/ collected on this workload:
+    the newest (round tags sort by name) profiled on this tree if there is one, else the newest."""
     import glob
-    best = None
+    best = same = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
         try:
             doc = json.load(open(path))
@@ -976,7 +976,19 @@ def pmc_doc(pattern, W, H, N):
         if (c.get("width"), c.get("height"), c.get("nfeatures")) == (W, H, N) and c.get("batch") \
                 and isinstance(doc.get("kernels"), dict):
             best = (path, doc)
-    return best
+            if pmc_tree(doc)["this_tree"]:
+                same = best
+    return same or best
+
+
+def pmc_tree(doc):
+    """The profiled tree a PMC document records (tools/profile_final.sh) and whether it is this one:
+    the library sources' hash (build.source_hash, the build id the loaded library is checked against)."""
+    t = doc.get("tree") if isinstance(doc, dict) else None
+    if not t:
+        return {"git": None, "this_tree": False}
+    from droplet_visual_odometry_amd.build import source_hash
+    return {"git": t.get("git"), "source_hash": t.get("source_hash"), "this_tree": t.get("source_hash") == source_hash()}
 
 
 def kernels_of(stage, names):
@@ -1006,12 +1018,13 @@ def pmc_counts(stage, W, H, N, B):
         return None
     scale = B / c["batch"] if stage in PAIR_STAGES else (B + 1) / (c["batch"] + 1)
     tot = lambda key: sum(doc["kernels"][k].get(key, 0.0) for k in ks)  # noqa: E731
-    src = f"profiles/{os.path.basename(path)} (rocprofv3 --pmc passes at batch {c['batch']}"
+    src = f"profiles/{os.path.basename(path)} (rocprofv3 --pmc passes at batch {c['batch']}, {c.get('streams', 1)} " \
+          f"stream(s)"
     src += ")" if c["batch"] == B else f", scaled per unit to batch {B})"
     return {"traffic": round((tot("fetch_bytes") + tot("write_bytes")) * scale),
             "traffic_raw": round((tot("fetch_bytes_raw") + tot("write_bytes_raw")) * scale),
             "calibrated": all(bool(doc["kernels"][k].get("calibrated")) for k in ks),
-            "valu_insts": tot("SQ_INSTS_VALU") * scale, "kernels": ks, "source": src}
+            "valu_insts": tot("SQ_INSTS_VALU") * scale, "kernels": ks, "source": src, "tree": pmc_tree(doc)}
 
 
 def ransac_f64(ms_per_launch, W, H, N, B):
@@ -1035,8 +1048,17 @@ def ransac_f64(ms_per_launch, W, H, N, B):
     # issue view: a wave64 f64 instruction holds a SIMD's f64 pipe 4 cycles (16 lanes per cycle)
     issue = insts * 4 / (ms_per_launch * 1e-3 * 1024 * 2.4e9)
     per_kernel = {k: round(v["f64_wave_insts"] * scale) for k, v in sorted(ks.items())}
+    # the lane pass (SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64) per kernel): FLOPs of active lanes only
+    weighted = None
+    if all("f64_flops_lane_weighted" in v for v in ks.values()):
+        weighted = sum(v["f64_flops_lane_weighted"] for v in ks.values()) * scale / (ms_per_launch * 1e-3) / 1e12
     return {"bound": "f64 valu", "achieved": round(achieved, 3), "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / F64_PEAK_TFLOPS, 5), "issue_frac": round(issue, 5),
+            "frac": round(achieved / F64_PEAK_TFLOPS, 5),
+            "frac_counts": "issued lane slots: every lane of every issued f64 wave-instruction",
+            "achieved_lane_weighted": round(weighted, 3) if weighted is not None else None,
+            "frac_lane_weighted": round(weighted / F64_PEAK_TFLOPS, 5) if weighted is not None else None,
+            "lane_util": {k: round(v["valu_lane_util"], 4) for k, v in sorted(ks.items()) if "valu_lane_util" in v},
+            "issue_frac": round(issue, 5), "tree": pmc_tree(doc),
             "f64_wave_insts_per_launch": round(insts), "f64_wave_insts_per_kernel": per_kernel,
             "f64_flops_per_launch": round(flops), "ms_per_launch": round(ms_per_launch, 4),
             "kernels": sorted(ks), "source": f"profiles/{os.path.basename(path)} (batch {c['batch']}, scaled per "
@@ -1063,6 +1085,7 @@ def hbm_roofline(stage, ms, W, H, N, B, m_avg):
             "traffic_raw": pmc["traffic_raw"] if pmc else None,
             "traffic_calibrated": pmc["calibrated"] if pmc else None,
             "traffic_source": pmc["source"] if pmc else None,
+            "traffic_tree": pmc["tree"] if pmc else None,
             "valu": valu, "valu_frac": valu["frac"] if valu else None,
             "stage": stage, "kernel": ", ".join(pmc["kernels"]) if pmc else " / ".join(STAGE_KERNELS[stage]),
             "algorithmic_bytes_per_launch": bytes_per_launch, "kernel_ms_per_launch": round(ms, 4),
@@ -1088,7 +1111,8 @@ def roofline_of(per_call, value, W, H, N, B, m_avg):
         pmc = pmc_counts("ransac", W, H, N, B)
         roof = {"bound": "f64", "achieved": rf["achieved"], "peak": rf["peak"], "unit": "TFLOP/s",
                 "frac": rf["frac"], "traffic": pmc["traffic"] if pmc else None,
-                "traffic_source": pmc["source"] if pmc else None, "stage": "ransac",
+                "traffic_source": pmc["source"] if pmc else None, "traffic_tree": pmc["tree"] if pmc else None,
+                "frac_counts": rf["frac_counts"], "frac_lane_weighted": rf["frac_lane_weighted"], "stage": "ransac",
                 "kernel": "RANSAC group: " + ", ".join(rf["kernels"]), "kernel_ms_per_launch": rf["ms_per_launch"],
                 "note": "dominant stage = most HIP-event time per step; the RANSAC group is scalar f64 work "
                         "(5-point solve, Durand-Kerner, Sampson scoring), priced against the 78.6 TFLOP/s FP64 "

@@ -70,7 +70,9 @@ def main(fetch, write, sq, calib, dst, batch=1024, rdreq=None):
         # the workload the passes ran (tools/profile_round.sh WL=...): DVO_PMC_CONFIG="width height nfeatures"
         "config": dict(zip(("width", "height", "nfeatures"),
                            (int(v) for v in os.environ.get("DVO_PMC_CONFIG", "1280 720 2000").split())),
-                       batch=int(batch), streams=1),
+                       batch=int(batch), streams=int(os.environ.get("DVO_PMC_STREAMS", "1"))),
+        # the profiled tree (tools/profile_final.sh): git commit and the library's source hash
+        "tree": json.loads(os.environ["DVO_PMC_TREE"]) if os.environ.get("DVO_PMC_TREE") else None,
         "unit": "per launch: bytes (FETCH_SIZE/WRITE_SIZE KB x1024, then the width calibration), "
                 "SQ_* instruction counts (wave-level)",
         "note": "separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ instruction counts); per batch launch: the "
