@@ -29,6 +29,11 @@ namespace {
 __constant__ int8_t c_pattern[256 * 4] = {
 #include "../../data/orb_bit_pattern_31.inc"
 };
+// the same points as floats (x0, y0, x1, y1 per pair): describe_kernel's lanes load theirs as float4s
+// instead of converting bytes per keypoint
+__constant__ __attribute__((aligned(16))) float c_pattern_f[256 * 4] = {
+#include "../../data/orb_bit_pattern_31.inc"
+};
 
 // ICAngles u_max for halfPatchSize 15 (orb.cpp computeKeyPoints): cvRound of
 // sqrt(225 - v^2) for v <= 11, then the symmetry fix-up; pinned by a test.
@@ -1509,7 +1514,8 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // the 16 IC-angle row segments of the unblurred level (registers) and the
 // blurred 39 x 44 window around it (word loads into LDS); the 512 rBRIEF
 // samples are then LDS reads.
-constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 44;  // pattern radius <= 13*sqrt(2) -> 19
+// pattern radius <= 13*sqrt(2) -> 19; rows of 64 bytes: a sample's offset is (iy << 6) + ix (phase 3)
+constexpr int kDPR = 19, kDPH = 2 * kDPR + 1, kDPW = 64;
 // keypoints per wave, the loads of all of them requested first.  Reading a blurred pyramid: 1 73.0 K,
 // 2 73.6 K, 4 72.3 K frames/s (profiles/r02z_ab_describe_dkw.txt); blurring the windows here
 // (16 raw rows per lane and keypoint): 1 74.8 K (51 VGPRs), 2 74.3 K (119 VGPRs), against 73.2 K
@@ -1543,10 +1549,18 @@ constexpr int kDBRow0 = 1;                                     // patch row of b
 constexpr int kDBBase[kDBSeg + 1] = {0, 11, 23, 35, 47, 56};    // first lane of each band
 constexpr int kDBHalfW[kDBSeg] = {15, 18, 18, 18, 12};          // largest |dx| in the band
 
+// Every stored word lies left of the level's last w % 4 columns (keypoints >= 31 pixels from the border,
+// the window <= 22 + a word): the half-to-even rule throughout.  The rounded sums s >> 16 are <= 257
+// (the 8-bit kernel sums to 257^2 > 2^16): v_sat_pk_u8_i16 saturates two of them to bytes.
+__device__ __forceinline__ uint32_t sat_pk_u8(uint32_t v) {
+    uint32_t d;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(d) : "v"(v));
+    return d;
+}
 __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw], uint8_t* patch_slot, int s, int wc,
-                                                   bool he, bool st) {
+                                                   bool st) {
     const u16x2 k18 = {18, 18}, k34 = {34, 34}, k49 = {49, 49}, k55 = {55, 55};
-    const uint32_t R = he ? 0x7FFFu : 0x8000u;
+    const uint32_t R = 0x7FFFu;
     u16x2 lo[7], hi[7];
 #pragma unroll
     for (int r = 0; r < kDBRaw; ++r) {
@@ -1579,16 +1593,13 @@ __device__ __forceinline__ void describe_blur_rows(const uint32_t (&raw)[kDBRaw]
         s3 = __builtin_amdgcn_udot2(b, (u16x2){49, 55}, s3, false);
         s3 = __builtin_amdgcn_udot2(ar, (u16x2){49, 34}, s3, false);
         s3 = __builtin_amdgcn_udot2(br, (u16x2){18, 0}, s3, false);
-        s0 += __builtin_amdgcn_ubfe(s0, 16, he);
-        s1 += __builtin_amdgcn_ubfe(s1, 16, he);
-        s2 += __builtin_amdgcn_ubfe(s2, 16, he);
-        s3 += __builtin_amdgcn_ubfe(s3, 16, he);
-        s0 = min(s0, 0xFFFFFFu);
-        s1 = min(s1, 0xFFFFFFu);
-        s2 = min(s2, 0xFFFFFFu);
-        s3 = min(s3, 0xFFFFFFu);
-        const uint32_t word = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0C0C0602u),
-                                                    __builtin_amdgcn_perm(s1, s0, 0x0C0C0602u), 0x05040100u);
+        s0 += __builtin_amdgcn_ubfe(s0, 16, 1);
+        s1 += __builtin_amdgcn_ubfe(s1, 16, 1);
+        s2 += __builtin_amdgcn_ubfe(s2, 16, 1);
+        s3 += __builtin_amdgcn_ubfe(s3, 16, 1);
+        // (s0 >> 16, s1 >> 16) and (s2 >> 16, s3 >> 16) as 16-bit pairs, saturated to bytes
+        const uint32_t word = sat_pk_u8(__builtin_amdgcn_perm(s1, s0, 0x07060302u)) |
+                              (sat_pk_u8(__builtin_amdgcn_perm(s3, s2, 0x07060302u)) << 16);
         const int i = kDBRow0 + kDBRows * s + (r - 6);  // patch row
         if (st && s < kDBSeg && wc >= 1 && wc <= 11 && i < kDPH)
             reinterpret_cast<uint32_t*>(patch_slot + i * kDPW)[wc - 1] = word;
@@ -1638,10 +1649,10 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
     }
     const int nk = min(total, P.plan.kp_cap);
     if (bxi * kDKB >= nk) return;  // whole block idle (uniform)
-    // rBRIEF pattern words of this lane's 4 bits (independent of the keypoint: issued first)
-    uint32_t pat[4];
+    // rBRIEF pattern points of this lane's 4 bits (independent of the keypoint: issued first)
+    float4 pat[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const uint32_t*>(c_pattern)[q * 64 + lane];
+    for (int q = 0; q < 4; ++q) pat[q] = reinterpret_cast<const float4*>(c_pattern_f)[q * 64 + lane];
     // ICAngles disk membership of this lane's 16 samples (u = column, v = row): keypoint independent
     // keypoint (level, index, key) of this wave's 4 slots, keys requested together
     int lv[kDKW], ix[kDKW];
@@ -1722,8 +1733,7 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
 #pragma unroll
         for (int t = 0; t < 5; ++t) reinterpret_cast<uint32_t*>(&icw[wv][0][0])[64 * t + lane] = ivs[kk][t];
         const int db_wc = db_wcs[kk];
-        describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc,
-                           a0 + 4 * (db_wc - 1) + 4 <= P.plan.L[l].w, db_st);
+        describe_blur_rows(pvs[kk], &patch[slot][0][0], db_s, db_wc, db_st);
         __builtin_amdgcn_wave_barrier();
         // m10 = sum u * I, m01 = sum v * I over the disk (integer: any order)
         int m10, m01;
@@ -1772,22 +1782,35 @@ __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
         s_sa[threadIdx.x] = (float)sd;
     }
     __syncthreads();
-    // ---- phase 3: rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2)
+    // ---- phase 3: rBRIEF on the blurred level (orb.cpp computeOrbDescriptors, WTA_K 2).  cvRound of a
+    // rotated coordinate v (|v| < 20) by the rounding constant M = 1.5 * 2^23: the float sum v + M is
+    // M + cvRound(v) (round to nearest, ties to even, as cvRound), so its bit pattern is Mi + cvRound(v)
+    // and (Y << 6) + X of a sample's two sums is its patch offset + 65 Mi (mod 2^32): two integer
+    // operations per sample instead of two round-and-converts and a multiply.
+    constexpr float kRoundM = 12582912.0f;
+    constexpr uint32_t kRoundC = 65u * 0x4B400000u;  // 65 x the bit pattern of M, mod 2^32
+    static_assert(sizeof(patch) < 65536, "patch offsets");
+    const uint8_t* pbytes = &patch[0][0][0];
     for (int kk = 0; kk < kDKW; ++kk) {
         const int slot = wv * kDKW + kk;
         const int k = bxi * kDKB + slot;
         if (k >= nk) break;
         const float ca = s_ca[slot], sa = s_sa[slot];
-        const uint8_t* pc = &patch[slot][0][0] + s_pc[slot];
-        int t0[4], t1[4];
+        const uint32_t pc = (uint32_t)(slot * (kDPH + 2) * kDPW + s_pc[slot]) - kRoundC;
+        // (x, y) = (px ca - py sa, px sa + py ca) as packed products and one packed sum (-(py sa) is
+        // (-sa) py exactly), then + M
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 cs = {ca, sa}, nsc = {-sa, ca};
+        const auto at = [&](float px, float py) {
+            const f32x2 r = (cs * (f32x2){px, px} + nsc * (f32x2){py, py}) + (f32x2){kRoundM, kRoundM};
+            const uint32_t X = __float_as_uint(r.x), Y = __float_as_uint(r.y);
+            return (uint32_t)pbytes[(Y << 6) + X + pc];
+        };
+        uint32_t t0[4], t1[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int px0 = (int8_t)(pat[q] & 0xFF), py0 = (int8_t)((pat[q] >> 8) & 0xFF);
-            const int px1 = (int8_t)((pat[q] >> 16) & 0xFF), py1 = (int8_t)(pat[q] >> 24);
-            float x0 = px0 * ca - py0 * sa, y0 = px0 * sa + py0 * ca;
-            float x1 = px1 * ca - py1 * sa, y1 = px1 * sa + py1 * ca;
-            t0[q] = pc[cv_round_f(y0) * kDPW + cv_round_f(x0)];
-            t1[q] = pc[cv_round_f(y1) * kDPW + cv_round_f(x1)];
+            t0[q] = at(pat[q].x, pat[q].y);
+            t1[q] = at(pat[q].z, pat[q].w);
         }
         unsigned long long words[4];
 #pragma unroll

@@ -20,13 +20,14 @@ out="$root/gpurun_out/prof"
 mkdir -p "$out"
 B=${B:-3072}
 S=${S:-2}
+SP=${SP:-1}  # the counter passes: one stream (rocprofv3 --pmc serialises dispatches; with two streams their cross-stream waits stalled it)
 side="--cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0"
-pass="$WL --batch $B --streams $S --steps 1 --warmup 1 --runs 1 --no-profile $side"
+pass="$WL --batch $B --streams $SP --steps 1 --warmup 1 --runs 1 --no-profile $side"
 tree="{\"git\": \"${DVO_TREE:-unknown}\", \"source_hash\": \"$(cd "$root" && python3 -c 'from droplet_visual_odometry_amd.build import source_hash; print(source_hash())')\"}"
 if [ "$part" = merge ]; then
   python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_calib_rdreq.csv" > /dev/null
-  DVO_PMC_TREE="$tree" DVO_PMC_STREAMS=$S python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" $B "$out/${tag}_pmc_rdreq.csv"
-  DVO_PMC_TREE="$tree" DVO_PMC_STREAMS=$S DVO_PMC_LANES="$out/${tag}_pmc_lanes.csv" python3 "$root/tools/pmc_f64.py" "$out/${tag}_pmc_f64.csv" "$out/${tag}_pmc_f64.json" $B
+  DVO_PMC_TREE="$tree" DVO_PMC_STREAMS=$SP python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" $B "$out/${tag}_pmc_rdreq.csv"
+  DVO_PMC_TREE="$tree" DVO_PMC_STREAMS=$SP DVO_PMC_LANES="$out/${tag}_pmc_lanes.csv" python3 "$root/tools/pmc_f64.py" "$out/${tag}_pmc_f64.csv" "$out/${tag}_pmc_f64.json" $B
   DVO_PMC_TREE="$tree" python3 "$root/tools/dk_passes.py" "$out/${tag}_f64_raw.csv" "$out/${tag}_kt_raw.csv" "$out/${tag}_dk_passes.json" "$out/${tag}_lanes_raw.csv" > "$out/${tag}_dk_passes.txt"
   exit 0
 fi
