@@ -9,6 +9,8 @@
 #      instruction) and a counter-free kernel trace for the Durand-Kerner per-pass durations;
 #   merge  -> gpurun_out/prof/<tag>_{pmc_traffic,pmc_f64,dk_passes}.json, each carrying the tree
 #      (DVO_TREE, the git commit, passed in by the caller) and the library's source hash.
+# Counter passes collect on the library's kernels only (--kernel-include-regex dvo::): the synthetic
+# frames are rendered by torch kernels, which counter collection would serialise one by one.
 # Every counter pass runs the bench with its timed step, priming and drain: per-launch figures are
 # the run's totals over its batch launches (normalize_kernel dispatches), so the pipeline's ramp
 # and drain rounds are counted with the batches they belong to.
@@ -35,7 +37,7 @@ export TMPDIR=/tmp
 cd /tmp
 run_pass() {  # name counters...
   local name=$1; shift
-  timeout -s KILL 170 rocprofv3 --pmc "$@" -d /tmp/pmc_${tag}_$name -o run --output-format csv -- python3 "$root/bench.py" $pass > "$out/${tag}_pmc_$name.log" 2>&1
+  timeout -s KILL 170 rocprofv3 --pmc "$@" --kernel-include-regex 'dvo::' -d /tmp/pmc_${tag}_$name -o run --output-format csv -- python3 "$root/bench.py" $pass > "$out/${tag}_pmc_$name.log" 2>&1
   python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_$name -name '*counter_collection.csv') "$out/${tag}_pmc_$name.csv" > /dev/null
 }
 calib_pass() {  # name counters...
