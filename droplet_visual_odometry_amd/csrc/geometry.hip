@@ -1334,6 +1334,7 @@ __global__ void dk_stats_kernel(int round, int nwaves) {
 #else
 #define DK_STAT(pass, n) ((void)0)
 #endif
+// 3 waves per SIMD (130 VGPRs); 4 spills 14 VGPRs and measured -0.3 % (profiles/r05s_ab_replay_dk_waves.txt)
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
     // pass 0: items [0, dk_ctl[1]) of the round's work list; pass k > 0: dk_list[k - 1][0, dk_ctl[1 + k])
@@ -1754,7 +1755,14 @@ __global__ __launch_bounds__(kScoreNT) void ransac_score_kernel(GeomArgs g, int 
 // nothing changes niters between events, so the loop ends at the first
 // hypothesis at or past niters.  Identical to the per-hypothesis loop
 // (which remains for rounds with more events than the event list holds).
-constexpr int kReplayNT = 64, kReplayMax = 1024, kReplayEv = 256;
+// kReplayMax: hypotheses per LDS chunk.  A pipelined round holds at most 32 / 32 / 64 / 128 hypotheses
+// per pair before the last one, so chunks of 256 (12 KB of LDS: 13 blocks per CU) rarely split a
+// round, where 1024 (46 KB: 3 blocks per CU) left the replay at under a wave per SIMD (RANSAC stage
+// 13.8 vs 13.9-14.5 ms per two-stream step, frames/s within noise: profiles/r05s_ab_replay_dk_waves.txt).
+#ifndef DVO_REPLAY_MAX
+#define DVO_REPLAY_MAX 256
+#endif
+constexpr int kReplayNT = 64, kReplayMax = DVO_REPLAY_MAX, kReplayEv = 256;
 __global__ __launch_bounds__(kReplayNT) void ransac_replay_kernel(GeomArgs g) {
     const int p = blockIdx.x;
     RansacState* Sp = g.rs + p;

@@ -1,0 +1,15 @@
+# replay chunks of 256 hypotheses (base) vs 1024 (r1024); Durand-Kerner at 4 waves/SIMD (dk4, 14 VGPRs spilled)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r05s
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r05s/gpu_tests.log 2>&1 || exit 1
+for t in base r1024 dk4 base r1024 dk4; do
+  lib=droplet_visual_odometry_amd/lib/libdvo_hip.so; [ "$t" != base ] && lib=droplet_visual_odometry_amd/lib/exp/libdvo_$t.so
+  DVO_LIB_PATH=$PWD/$lib timeout -k 10 300 python -u bench.py --steps 12 --warmup 5 --runs 3 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0 > gpurun_out/r05s/d_$t.json 2> gpurun_out/r05s/d_$t.err || exit 1
+  python3 -c "
+import json
+d=json.loads([l for l in open('gpurun_out/r05s/d_$t.json') if l.startswith('{')][-1])
+st=d['roofline']['stage_ms_per_step']
+print('$t', d['value'], d['ms_per_step'], d['runs']['frames_per_s'], 'pyramid', st.get('pyramid'), 'ransac', st.get('ransac'))" >> gpurun_out/r05s/ab.txt
+done
