@@ -39,8 +39,9 @@ sys.path.insert(0, ROOT)
 # share a queue run in order, so the copy stream of the host-fed leg queued behind a library stream's
 # kernels (host-fed 45.0 K -> 58.1 K frames/s with 8; the device-resident run is unchanged,
 # profiles/r05h_queues.txt).  The bench runs two library streams, torch's stream, a side stream and a
-# copy stream: 8 queues give each its own.  Set before the HIP runtime starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# copy stream: 8 queues give each its own.  Set before the HIP runtime starts, over the environment's
+# value (the GPU box exports HIP's default, 4); DVO_BENCH_HW_QUEUES chooses another count.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DVO_BENCH_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # VALU issue: a SIMD issues one wave64 VALU instruction per 2 cycles; 256 CUs x 4 SIMDs at 2.4 GHz
@@ -674,17 +675,18 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
     T_abs = [torch.empty((N * B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
     cur = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
-    done = [None] * S
+    done = {}  # record buffer -> the event after its last read (the stand-in collective)
 
     def on_retire(k, r, pairs, s0):
         fs = pipe.fss[k]
         cur.wait_event(fs.record_event())  # the records are final (before the collective)
         # stands in for the all-gather: it reads the records buffer, which the library rewrites only
-        # pipeline_depth() submits later, after waiting for this copy
+        # pipeline_depth() submits later, after waiting for this copy (as the runner's per-slot wait,
+        # dist.ShardedStreamRunner.step)
         wrecs[k][:pairs * rb].copy_(r[:pairs * rb])
         ev = torch.cuda.Event()
         ev.record(cur)
-        done[k] = ev
+        done[r.data_ptr()] = ev
         # rank 0's half of the split tail (dist.ShardedStreamRunner): T_rel of its own B pairs, then
         # (after the T_rel all-gather, stood in for by the window's T_rel buffer) the serial chain on
         # a host thread
@@ -696,7 +698,9 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
 
         def step(i):
             s0, k = (i % n_windows) * B, i % S
-            pipe.fss[k].wait_event(done[k])
+            nxt = pipe.recs[k][pipe.nsub[k] % pipe.D]  # the buffer this submit writes
+            if nxt.data_ptr() in done:
+                pipe.fss[k].wait_event(done[nxt.data_ptr()])
             pipe.step(k, pool[s0:s0 + B + 1], s0)
 
         prime = max(args.warmup, pipe.prime_steps)

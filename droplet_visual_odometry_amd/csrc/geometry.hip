@@ -1187,10 +1187,10 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, RoundSpec
 }
 
 // The five-point record of hypothesis h of launch pair p: records exist for the round's
-// hypotheses only, 64 per block, the pair's [h0, h1) from block a_off[p] on (so a stage A / C
-// block of 64 consecutive hypotheses writes one record block: coalesced).
+// hypotheses only, one per work item (dk_off[p] + h - h0), in blocks of 64 items (a wave of stage
+// A / C / Durand-Kerner pass 0 = 64 consecutive items = one record block: coalesced).
 __device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
-    const int64_t r = (int64_t)g.a_off[p] * 64 + (h - g.rs[p].h0);
+    const int64_t r = (int64_t)g.dk_off[p] + (h - g.rs[p].h0);
     return g.fprec + ((r >> 6) * kRecDoubles) * 64 + (r & 63);
 }
 
@@ -1256,17 +1256,33 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
     }
 }
 
-// Stage A of every hypothesis of the round (one thread each).
-// A 1-D grid over the round's 64-hypothesis blocks (a_off), sized for the largest round.
+// The launch pair of work item e = e0 + lane (dk_off: the round's hypotheses of all pairs back to
+// back), for the wave of items [e0, e0 + 64): the first item's pair by a wave-uniform binary search,
+// then the pair boundaries inside the wave (typically one or two: a round gives a pair 32+
+// hypotheses) by uniform loads, each lane counting those at or below its item (empty pairs repeat a
+// boundary and are counted through).  Packing the items leaves no lane idle where a pair's
+// hypotheses end (64-hypothesis blocks per pair left stage A at 0.61 and stage C at 0.24 of the
+// VALU lanes active, profiles/r05zz_pmc_f64.json).
+__device__ __forceinline__ int wave_item_pair(const int32_t* off, int pairs, int e0, int e) {
+    int p = pair_of(off, pairs, e0);
+    const int pb = p;
+    for (int k = pb + 1; k <= pairs; ++k) {
+        const int b = off[k];
+        if (b > e0 + 63) break;
+        p += e >= b;
+    }
+    return p;
+}
+
+// Stage A of every hypothesis of the round (one thread each), a 1-D grid over the round's items.
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_a_kernel(GeomArgs g, int pairs) {
-    const int b = blockIdx.x;
-    if (b >= g.a_off[pairs]) return;
-    const int p = pair_of(g.a_off, pairs, b);
-    const RansacState& S = g.rs[p];
-    const int h0 = S.h0, h1 = S.h1;
-    const int h = h0 + (b - g.a_off[p]) * kSolveNT + threadIdx.x;
+    const int e0 = blockIdx.x * kSolveNT;
+    if (e0 >= g.dk_off[pairs]) return;
+    const int e = e0 + threadIdx.x;
+    const int p = wave_item_pair(g.dk_off, pairs, e0, e);
     __shared__ double lds_g[36 * kSolveNT];
-    if (h >= h1) return;
+    if (e >= g.dk_off[pairs]) return;
+    const int h = g.rs[p].h0 + (e - g.dk_off[p]);
     const double* npts = g.npts + (int64_t)p * g.pts_stride * 4;
     const int32_t* idx = g.subsets + ((int64_t)p * g.hyp_cap + h) * 5;
     double q[5][4];
@@ -1517,13 +1533,12 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
 
 // Stage C of every hypothesis of the round: models and their count.
 __global__ __launch_bounds__(kSolveNT) void ransac_stage_c_kernel(GeomArgs g, int pairs) {
-    const int b = blockIdx.x;
-    if (b >= g.a_off[pairs]) return;
-    const int p = pair_of(g.a_off, pairs, b);
-    const RansacState& S = g.rs[p];
-    const int h0 = S.h0, h1 = S.h1;
-    const int h = h0 + (b - g.a_off[p]) * kSolveNT + threadIdx.x;
-    if (h >= h1) return;
+    const int e0 = blockIdx.x * kSolveNT;
+    if (e0 >= g.dk_off[pairs]) return;
+    const int e = e0 + threadIdx.x;
+    const int p = wave_item_pair(g.dk_off, pairs, e0, e);
+    if (e >= g.dk_off[pairs]) return;
+    const int h = g.rs[p].h0 + (e - g.dk_off[p]);
     g.nmod[(int64_t)p * g.hyp_cap + h] =
         fp_stage_c(hyp_record(g, p, h), g.models + ((int64_t)p * g.hyp_cap + h) * 90);
 }
@@ -1968,7 +1983,8 @@ static hipError_t launch_round(const GeomArgs& g, const RoundSpec& spec, bool on
     hipLaunchKernelGGL(ransac_sample_kernel, dim3(pairs), dim3(64), 0, s, g, spec);
     if (w.items == 0) return hipGetLastError();  // no pair of the launch can have a hypothesis
     hipLaunchKernelGGL(ransac_plan_kernel, dim3(1), dim3(1024), 0, s, g, pairs, sh);
-    hipLaunchKernelGGL(ransac_stage_a_kernel, dim3((unsigned)w.ablocks), dim3(kSolveNT), 0, s, g, pairs);
+    const dim3 agrid((unsigned)((w.items + kSolveNT - 1) / kSolveNT));
+    hipLaunchKernelGGL(ransac_stage_a_kernel, agrid, dim3(kSolveNT), 0, s, g, pairs);
     if (one) {
         hipLaunchKernelGGL(ransac_dk_wide_kernel, dim3((unsigned)((w.items + 3) / 4)), dim3(64), 0, s, g, pairs);
         int span = 0;  // the per-call path: one set, round 0 up to the cap
@@ -1984,7 +2000,7 @@ static hipError_t launch_round(const GeomArgs& g, const RoundSpec& spec, bool on
 #ifdef DVO_DK_STATS
         hipLaunchKernelGGL(dk_stats_kernel, dim3(1), dim3(1), 0, s, spec.round[0], (int)dgrid.x * (kDkNT / 64));
 #endif
-        hipLaunchKernelGGL(ransac_stage_c_kernel, dim3((unsigned)w.ablocks), dim3(kSolveNT), 0, s, g, pairs);
+        hipLaunchKernelGGL(ransac_stage_c_kernel, agrid, dim3(kSolveNT), 0, s, g, pairs);
         hipLaunchKernelGGL(ransac_score_kernel<kScoreHyps>, dim3((unsigned)w.sblocks), dim3(kScoreNT), 0, s, g,
                            pairs);
     }
