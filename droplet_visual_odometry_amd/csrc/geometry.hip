@@ -891,9 +891,14 @@ __device__ __forceinline__ int fp_stage_c(double* R, double* models) {
 #pragma unroll
     for (int k = 0; k < 36; ++k) EE[k] = R[(kRecEE + k) * 64];
     const int nr = (int)R[kRecNr * 64];
+    // the real roots first, as a mask: a wave then runs as many root models as its lane with the most
+    // real roots, not one per root position any lane's real root sits at
+    uint32_t real = 0;
+    for (int i = 0; i < nr; ++i) real |= (fabs(R[(kRecRoots + 2 * i + 1) * 64]) > 1e-10 ? 0u : 1u) << i;
     int count = 0;
-    for (int i = 0; i < nr; ++i) {
-        if (fabs(R[(kRecRoots + 2 * i + 1) * 64]) > 1e-10) continue;
+    while (real) {
+        const int i = __builtin_ctz(real);
+        real &= real - 1;
         double e[9];
         if (!root_model(b, EE, R[(kRecRoots + 2 * i) * 64], e)) continue;
         double* out = models + count * 9;
@@ -1189,9 +1194,11 @@ __global__ __launch_bounds__(64) void ransac_sample_kernel(GeomArgs g, RoundSpec
 // The five-point record of hypothesis h of launch pair p: records exist for the round's
 // hypotheses only, one per work item (dk_off[p] + h - h0), in blocks of 64 items (a wave of stage
 // A / C / Durand-Kerner pass 0 = 64 consecutive items = one record block: coalesced).
-__device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
-    const int64_t r = (int64_t)g.dk_off[p] + (h - g.rs[p].h0);
+__device__ __forceinline__ double* item_record(const GeomArgs& g, int64_t r) {
     return g.fprec + ((r >> 6) * kRecDoubles) * 64 + (r & 63);
+}
+__device__ __forceinline__ double* hyp_record(const GeomArgs& g, int p, int h) {
+    return item_record(g, (int64_t)g.dk_off[p] + (h - g.rs[p].h0));
 }
 
 // Pair of a round work-list item: the p with off[p] <= item < off[p + 1] (off ascending).
@@ -1360,8 +1367,7 @@ void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
     const int e = blockIdx.x * kDkNT + threadIdx.x;
     if (e >= total) return;
     const int item = pass == 0 ? e : g.dk_list[(int64_t)(pass - 1) * g.dk_list_cap + e];
-    const int lo = pair_of(g.dk_off, pairs, item);
-    double* R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
+    double* R = item_record(g, item);  // the item's record (no pair lookup: records are per item)
     if (pass == 0 && R[kRecGeneric * 64] != 0.0) return;  // stage C runs the generic solver
     double c[11];
 #pragma unroll
@@ -1461,8 +1467,7 @@ __global__ __launch_bounds__(64) void ransac_dk_wide_kernel(GeomArgs g, int pair
     bool active = item < total;
     double* R = nullptr;
     if (active) {
-        const int lo = pair_of(g.dk_off, pairs, item);
-        R = hyp_record(g, lo, g.rs[lo].h0 + (item - g.dk_off[lo]));
+        R = item_record(g, item);
         active = R[kRecGeneric * 64] == 0.0;  // else stage C runs the generic solver
     }
     if (__ballot(active) == 0) return;
