@@ -102,8 +102,16 @@ def parse():
     ap.add_argument("--tail-world", type=int, default=8,
                     help="rehearse rank 0's reassembly load of a world-N window at N=1: the pose tail and absolute "
                          "chain over N x B gathered records on torch's stream beside the library streams (0 = skip)")
-    ap.add_argument("--pose-check-32", type=int, default=24,
-                    help="pairs of the OpenCV 3.2-semantics pose check against the oracle (0 = skip)")
+    ap.add_argument("--pose-check-32", type=int, default=256,
+                    help="pairs of the OpenCV 3.2-semantics pose check against the oracle (0 = skip); run by the "
+                         "c3_ocv32 config leg when it is enabled")
+    ap.add_argument("--config-legs", default="c2,c5,c3_ocv32",
+                    help="BASELINE configs timed after the headline, each with the headline's pipelined two-stream "
+                         "schedule, roofline and an oracle pose check (comma list of c2, c5, c3_ocv32; 'none' skips)")
+    ap.add_argument("--leg-steps", type=int, default=10, help="timed steps per run of a config leg")
+    ap.add_argument("--leg-runs", type=int, default=3, help="timed runs of a config leg (value = the median)")
+    ap.add_argument("--leg-pose-pairs", type=int, default=64,
+                    help="pairs of a config leg's pose check against the oracle in the same semantics")
     ap.add_argument("--runs", type=int, default=5,
                     help="timed runs of exactly --steps steps each; value = the median run (BASELINE.md §3: "
                          "median of 5 runs), every run's rate reported under `runs`")
@@ -331,7 +339,7 @@ def main():
     sync_all()
     drain_ms = 1e3 * (time.perf_counter() - t_d)
     recs = FrameStream.records_numpy(*pipe.last)
-    rec_ref = pipe.last
+    pipe_depth, pipe_prime = pipe.D, pipe.prime_steps
     ms_per_step = 1000.0 * elapsed / args.steps
 
     m_avg = float(np.mean(recs["n_matches"])) if len(recs) else N / 2
@@ -397,10 +405,32 @@ def main():
         pose_check = {"pairs": n, "bit_identical": ident, "max_abs_R_err": err_r, "max_abs_t_err": err_t,
                       "ate_m": ate, "reference": "oracle/ C++ restatement, same frames; ATE = RMS position "
                                                  "difference of the marker-scaled chained trajectories"}
-        if args.pose_check_32 > 0:
+        leg_names = [x for x in args.config_legs.split(",") if x and x != "none"]
+        if args.pose_check_32 > 0 and "c3_ocv32" not in leg_names:
             pose_check_32 = pose_check_opencv32(pool, scene.K, N, args.max_iters, args.pose_check_32, ctx)
 
     dropin = dropin_rate(pool, corners, scene.K, N, args.dropin_seconds) if args.dropin_seconds > 0 else None
+
+    # BASELINE's other configs and the OpenCV 3.2 semantics, each on its own streams after the headline's
+    # are released (never `value`)
+    leg_names = [x for x in args.config_legs.split(",") if x and x != "none"]
+    if leg_names:
+        for f in fss:
+            f.close()
+        del pipe, fss, pool, corners, T_rel, T_abs
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        cfg_legs = {}
+        for name in leg_names:
+            try:
+                cfg_legs[name] = config_leg(args, ctx, dev, name)
+            except Exception as e:  # noqa: BLE001
+                cfg_legs[name] = {"error": f"{type(e).__name__}: {e}"}
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        if "c3_ocv32" in cfg_legs and "pose_check" in cfg_legs["c3_ocv32"]:
+            pose_check_32 = cfg_legs["c3_ocv32"]["pose_check"]
+        legs["configs"] = cfg_legs
 
     default_cfg = (W, H, N) == (1280, 720, 2000)
     out = {
@@ -424,7 +454,7 @@ def main():
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0,
                    "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0,
-                   "ransac_pipeline": {"depth": pipe.D, "prime_steps": max(args.warmup, pipe.prime_steps),
+                   "ransac_pipeline": {"depth": pipe_depth, "prime_steps": max(args.warmup, pipe_prime),
                                        "drain_ms": round(drain_ms, 3),
                                        "note": "RANSAC rounds of the last `depth` batches of a stream run as one "
                                                "merged round per submit (include/dvo.h dvo_stream_submit); after "
@@ -437,7 +467,6 @@ def main():
         "pose_check_opencv32": pose_check_32,
         "runs": runs,
         "dropin": dropin,
-        "legs": legs,
     }
     if cpu is not None:
         out["speedup_vs_cpu_same_mode"] = {"streaming": round(value / max(cpu["value"], 1e-9), 1)}
@@ -445,6 +474,7 @@ def main():
             out["speedup_vs_cpu_same_mode"]["reference_equivalent"] = \
                 legs["reference_equivalent"]["speedup_vs_cpu_same_mode"]
         out["speedup_vs_cpu_same_mode"]["cpu_threads"] = cpu["cores"]
+    out["legs"] = legs  # last: the config legs' summaries end the line
     print(json.dumps(out), flush=True)
 
 
@@ -749,12 +779,62 @@ def rank0_tail_leg(args, pool, pipe, corners, n_windows, K, ctx):
                     "per rank (weak scaling)"}
 
 
+def oracle_pairs(host, K, nfeatures, max_iters, n_pairs, semantics):
+    """The oracle's R, t for pairs 0 .. n_pairs-1 of a frame stream (host(i) = frame i as numpy), in
+    streaming mode (each frame's features reused by the next pair), over all usable host threads: the
+    pairs split into contiguous runs, each starting with a fresh detect of its first frame (detection is
+    a function of the frame, so this equals one sequential pass).  ctypes releases the GIL inside the
+    oracle's C++ calls.  Returns [(R or None, t_unit, n_matches)] in pair order."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.use_native_build()
+    T = max(1, min(cpu_threads(), n_pairs))
+    bounds = [(n_pairs * t // T, n_pairs * (t + 1) // T) for t in range(T)]
+    frames = [host(i) for i in range(n_pairs + 1)]
+    out = [None] * n_pairs
+    errors = []
+
+    def worker(a, b):
+        try:
+            kp = oracle.detect_and_compute(frames[a], nfeatures, semantics=semantics)
+            for i in range(a, b):
+                r = oracle.pair_pose(frames[i], frames[i + 1], K, nfeatures, max_iters=max_iters, kp_prev=kp,
+                                     semantics=semantics)
+                kp = (r["kp_cur"], r["desc_cur"])
+                out[i] = (r["R"], r["t_unit"], len(r["q"]) if r.get("q") is not None else None)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ths = [threading.Thread(target=worker, args=ab) for ab in bounds if ab[1] > ab[0]]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    if errors:
+        raise errors[0]
+    return out, T
+
+
+def compare_records(g, ref, check_matches=False):
+    """Pairs whose device record equals the oracle's R and t bit for bit (a pair the oracle fails must fail
+    on the device too); with check_matches the cross-checked match count as well."""
+    ident = 0
+    for i, (R, t, nm) in enumerate(ref):
+        if R is None:
+            ident += int(g["status"][i] != 0)
+            continue
+        ident += int(g["status"][i] == 0 and np.array_equal(g["R"][i].reshape(3, 3), R)
+                     and np.array_equal(g["t"][i], np.asarray(t).ravel())
+                     and (not check_matches or g["n_matches"][i] == nm))
+    return ident
+
+
 def pose_check_opencv32(pool, K, nfeatures, max_iters, n_pairs, ctx):
     """OpenCV 3.2 semantics (FrameStream(opencv="3.2"): INTER_LINEAR pyramid,
     3.2 retainBest, 3.x reverse-pass cross check) on the first n_pairs of the
     same stream, against the oracle in the same mode (streaming, features
     reused)."""
-    import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from droplet_visual_odometry_amd.stream import FrameStream
@@ -765,23 +845,111 @@ def pose_check_opencv32(pool, K, nfeatures, max_iters, n_pairs, ctx):
     fs.sync()
     g = FrameStream.records_numpy(rec, n)
     fs.close()
-    host = lambda i: pool[i].cpu().numpy()  # noqa: E731
-    kp = oracle.detect_and_compute(host(0), nfeatures, semantics=oracle.OCV32)
-    ident = 0
-    for i in range(n):
-        r = oracle.pair_pose(host(i), host(i + 1), K, nfeatures, max_iters=max_iters, kp_prev=kp,
-                             semantics=oracle.OCV32)
-        kp = (r["kp_cur"], r["desc_cur"])
-        if r["R"] is None:
-            ident += int(g["status"][i] != 0)
-            continue
-        ident += int(g["status"][i] == 0 and g["n_matches"][i] == len(r["q"])
-                     and np.array_equal(g["R"][i].reshape(3, 3), r["R"])
-                     and np.array_equal(g["t"][i], r["t_unit"].ravel()))
-    del torch
-    return {"pairs": n, "bit_identical": ident,
+    ref, T = oracle_pairs(lambda i: pool[i].cpu().numpy(), K, nfeatures, max_iters, n, oracle.OCV32)
+    return {"pairs": n, "bit_identical": compare_records(g, ref, check_matches=True),
             "reference": "oracle/ in OpenCV 3.2 mode (INTER_LINEAR pyramid, 3.2 retainBest, 3.x cross check), "
-                         "same frames, streaming"}
+                         f"same frames, streaming ({T} threads)"}
+
+
+# BASELINE.json configs timed as legs (north_star: 640x480 and 1280x720 numbers; configs[4] on one GPU) and the
+# headline config in OpenCV 3.2 semantics, the version the reference most likely ran
+CONFIG_LEGS = {
+    "c2": dict(width=640, height=480, nfeatures=1000, batch=3072, max_iters=1000, opencv="4.x"),
+    "c5": dict(width=1920, height=1080, nfeatures=4000, batch=1024, max_iters=4096, opencv="4.x"),
+    "c3_ocv32": dict(width=1280, height=720, nfeatures=2000, batch=3072, max_iters=1000, opencv="3.2"),
+}
+
+
+def config_leg(args, ctx, dev, name):
+    """One BASELINE config through the headline's schedule: S streams of pipelined submits
+    (Pipeline), the pose tail on every retired batch, prime_steps untimed submits, then
+    --leg-runs runs of exactly --leg-steps steps (value = the median run), HIP-event stage times
+    -> the dominant stage's roofline, and the first pairs of window 0 (pipelined submit + drain)
+    against the oracle in the same semantics, bit for bit."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from droplet_visual_odometry_amd.stream import FrameStream
+    from droplet_visual_odometry_amd.synth import MARKER_LEN, SceneStream
+    c = CONFIG_LEGS[name]
+    W, H, N, B, it = c["width"], c["height"], c["nfeatures"], c["batch"], c["max_iters"]
+    S = max(1, args.streams)
+    t_leg = time.perf_counter()
+    scene = SceneStream(W, H, device=str(dev))
+    pool_n = 2 * B + 1
+    pool = torch.stack([scene.render(i) for i in range(pool_n)]).contiguous()
+    corners = torch.tensor(np.stack([scene.marker_corners(i) for i in range(pool_n)]), dtype=torch.float64,
+                           device=dev)
+    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=it, ctx=ctx, opencv=c["opencv"])
+           for _ in range(S)]
+    for f in fss[1:]:
+        f.share_pose(fss[0])
+    T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    fss[0].reset_pose()
+    pipe = Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
+    torch.cuda.synchronize()
+    n_windows = 2
+
+    def step(i):
+        s0 = (i % n_windows) * B
+        pipe.step(i % S, pool[s0:s0 + B + 1], s0)
+
+    prime = max(args.warmup, pipe.prime_steps)
+    for i in range(prime):
+        step(i)
+    pipe.sync()
+    for f in fss:
+        f.set_profiling(True)
+    la = argparse.Namespace(runs=args.leg_runs, steps=args.leg_steps)
+    per_run = timed_runs(la, step, pipe.sync, prime)
+    value, runs = runs_summary(per_run, B * args.leg_steps)
+    stage_ms, calls = {}, 0
+    for f in fss:
+        sm, cc = f.stage_times()
+        calls += cc
+        for kk, v in sm.items():
+            stage_ms[kk] = stage_ms.get(kk, 0.0) + v
+        f.set_profiling(False)
+    pipe.drain()
+    pipe.sync()
+    recs = FrameStream.records_numpy(*pipe.last)
+    m_avg = float(np.mean(recs["n_matches"]))
+    roof = roofline_of({k: v / calls for k, v in stage_ms.items()}, value, W, H, N, B, m_avg) if calls else None
+    # window 0's first pairs through the pipelined submit, against the oracle in the same semantics
+    n = min(args.pose_check_32 if name == "c3_ocv32" else args.leg_pose_pairs, B)
+    rec0 = fss[0].new_records(B)
+    torch.cuda.synchronize()
+    fss[0].submit(pool[0:B + 1], rec0, wait_torch=False)
+    fss[0].drain()
+    fss[0].sync()
+    g = FrameStream.records_numpy(rec0, B)
+    sem = oracle.OCV32 if c["opencv"] == "3.2" else oracle.OCV4
+    t_o = time.perf_counter()
+    ref, T = oracle_pairs(lambda i: pool[i].cpu().numpy(), scene.K, N, it, n, sem)
+    oracle_s = time.perf_counter() - t_o
+    ident = compare_records(g, ref, check_matches=True)
+    for f in fss:
+        f.close()
+    del pipe, fss, pool, corners, T_rel, T_abs
+    torch.cuda.empty_cache()
+    out = {"value": round(value, 1), "unit": "frames/s", "config": f"{W}x{H} N{N} it{it} B{B} x{S} streams, OpenCV "
+           f"{c['opencv']}", "ms_per_step": round(1e3 * B / value, 3), "runs": {"median": runs["median"],
+           "spread_frac": runs["spread_frac"], "n": runs["n"], "steps": args.leg_steps},
+           "mean_hypotheses_solved": round(float(np.mean(recs["n_hypotheses"])), 1),
+           "mean_ransac_iters": round(float(np.mean(recs["ransac_iters"])), 1),
+           "pairs_ok": f"{int(np.sum(recs['status'] == 0))}/{len(recs)}",
+           "pose_check": {"pairs": n, "bit_identical": ident, "oracle_threads": T, "oracle_s": round(oracle_s, 1),
+                          "semantics": c["opencv"]},
+           "leg_s": round(time.perf_counter() - t_leg, 1)}
+    if roof:
+        hd = roof.get("hbm_dominant") or {}
+        out["roofline"] = {"dominant_stage": roof["dominant_stage"], "bound": roof["bound"],
+                           "frac": roof["frac"], "unit": roof["unit"], "achieved": roof["achieved"],
+                           "path_frac": roof["path_frac"],
+                           "hbm_dominant": {"stage": hd.get("stage"), "frac": hd.get("frac")} if hd else None,
+                           "stage_ms_per_step": roof["stage_ms_per_step"]}
+    return out
 
 
 def main_sharded(args, world, rank, local_rank, backend, dev, scene):

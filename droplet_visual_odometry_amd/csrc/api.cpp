@@ -89,6 +89,8 @@ struct dvo_stream {
         dvo_pair_record* rec = nullptr;  // the caller's records of the batch
     };
     PairSet sets[kMaxSets];
+    int nsets = 0;  // pair sets allocated: 1 until the first submit, then kRansacRounds (alloc_sets)
+    std::vector<void*> set_allocs;  // their buffers (also in allocs)
     int next_set = 0;  // the set the next submit fills (sets are taken in ring order)
     int last_set = 0;  // the set of the last submitted batch (get_matches)
     int retired = 0;   // batches retired by the last submit / drain / process call
@@ -453,6 +455,53 @@ GeomArgs geom_set(const GeomArgs& g, int k, int F, int64_t hc) {
 // Row pitch of the internal frame slab (word-aligned rows for the byte kernels).
 int frame_pitch(const dvo_stream* s) { return (s->cfg.width + 15) & ~15; }
 
+// The per-pair geometry, one copy per pair set.  A stream starts with one set: the
+// drained calls (dvo_stream_process, _process_pairs, _pair) run a batch's rounds back to back
+// in it.  The first dvo_stream_submit / _submit_pairs grows it to kRansacRounds sets (the
+// pipeline depth); no set is occupied then, since every drained call retires what it started.
+// At 1280x720, N 2000, maxIters 1000 a set costs about 0.9 MB per pair (models 720 KB of it).
+int alloc_sets(dvo_stream* s, int nsets) {
+    dvo_ctx* ctx = s->ctx;
+    Buffers& b = s->buf;
+    if (!s->set_allocs.empty()) {
+        HIP_TRY(hipStreamSynchronize(s->hs));
+        for (void* q : s->set_allocs) {
+            hipFree(q);
+            s->allocs.erase(std::find(s->allocs.begin(), s->allocs.end(), q));
+        }
+        s->set_allocs.clear();
+    }
+    const size_t first = s->allocs.size();
+    const size_t SF = (size_t)nsets * s->cfg.max_frames;
+    const int cap = s->plan.kp_cap;
+    const size_t hc = (size_t)(s->cfg.max_iters > 1 ? s->cfg.max_iters : 1);
+    int rc = DVO_OK;
+    auto take = [&](auto*& ptr, size_t n) {
+        if (!rc) rc = dalloc(s, &ptr, n);
+    };
+    take(b.nmatch, SF);
+    take(b.pts, SF * cap * 4);
+    take(b.npts, SF * cap * 4);
+    take(b.models, SF * hc * 90);
+    take(b.nmod, SF * hc);
+    take(b.rcnt, SF * hc * 10);
+    take(b.subsets, SF * hc * 5);
+    take(b.rs, SF);
+    take(b.hdr, SF);
+    take(b.dk_off, SF + 1);
+    take(b.a_off, SF + 1);
+    take(b.s_off, SF + 1);
+    take(b.E, SF * 90);
+    take(b.info, SF * 4);
+    take(b.Rt, SF * 12);
+    take(b.good, SF);
+    take(b.pose_P, SF * 72);
+    take(b.pose_cnt, SF * 5);
+    s->set_allocs.assign(s->allocs.begin() + first, s->allocs.end());
+    s->nsets = rc ? 0 : nsets;
+    return rc;
+}
+
 int stream_alloc(dvo_stream* s) {
     const int F = s->cfg.max_frames;
     const Plan& p = s->plan;
@@ -480,32 +529,14 @@ int stream_alloc(dvo_stream* s) {
     A(b.mq, (size_t)F * cap);
     A(b.mt, (size_t)F * cap);
     A(b.md, (size_t)F * cap);
-    // per-pair geometry: one copy per pair set (kRansacRounds batches in flight)
-    const size_t SF = (size_t)kRansacRounds * F;
-    A(b.nmatch, SF);
-    A(b.pts, SF * cap * 4);
-    A(b.npts, SF * cap * 4);
     const size_t hc = (size_t)(s->cfg.max_iters > 1 ? s->cfg.max_iters : 1);
-    A(b.models, SF * hc * 90);
-    A(b.nmod, SF * hc);
-    A(b.rcnt, SF * hc * 10);
-    A(b.subsets, SF * hc * 5);
-    A(b.rs, SF);
-    A(b.hdr, SF);
-    // five-point records and parked Durand-Kerner lists of one merged round
+    if ((rc = alloc_sets(s, 1))) return rc;
+    // five-point records and parked Durand-Kerner lists of one merged round (a bound over any
+    // number of sets: one set at each round)
     A(b.fprec, (size_t)std::max<int64_t>(round_blocks_bound(F, (int)hc), (int64_t)(hc + 63) / 64) * 128 * 64);
-    A(b.dk_off, SF + 1);
-    A(b.a_off, SF + 1);
-    A(b.s_off, SF + 1);
     A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
     A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
-    A(b.E, SF * 90);
-    A(b.info, SF * 4);
-    A(b.Rt, SF * 12);
-    A(b.good, SF);
-    A(b.pose_P, SF * 72);
-    A(b.pose_cnt, SF * 5);
     A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
     A(s->d_carry, (size_t)28);
 #undef A
@@ -573,10 +604,10 @@ int collect_events(dvo_stream* s) {
 int merged_round(dvo_stream* s) {
     dvo_ctx* ctx = s->ctx;
     RoundSpec sp{};
-    sp.nsets = kRansacRounds;
+    sp.nsets = s->nsets;
     sp.F = s->cfg.max_frames;
     bool any = false;
-    for (int k = 0; k < kRansacRounds; ++k) {
+    for (int k = 0; k < s->nsets; ++k) {
         auto& st = s->sets[k];
         const bool run = st.used && st.round < kRansacRounds;
         sp.round[k] = run ? st.round : -1;
@@ -637,6 +668,12 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     s->retired = 0;
     s->last_has_pairs = false;  // set again when a batch retires: the pose tail reads its records
     const int F = s->cfg.max_frames;
+    if (pairs >= 1 && !drain && s->nsets < kRansacRounds) {  // the first pipelined submit: grow the sets
+        if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "pair sets occupied at the first submit");
+        int rc = alloc_sets(s, kRansacRounds);
+        if (rc) return rc;
+        s->next_set = 0;
+    }
     const int k = s->next_set;
     if (pairs >= 1 && s->sets[k].used) {  // the ring is full (cannot happen in lockstep): finish its oldest
         int rc;
@@ -664,7 +701,7 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
         HIP_TRY(launch_geometry_args(geom_set(g, k, F, g.hyp_cap), pairs, kStageNormalize, s->hs));
         s->sets[k] = dvo_stream::PairSet{true, 0, pairs, d_rec};
         s->last_set = k;
-        s->next_set = (k + 1) % kRansacRounds;
+        s->next_set = (k + 1) % s->nsets;
     }
     if (pairs < 1 && !drain) return DVO_OK;
     int rc;
@@ -870,6 +907,7 @@ int dvo_pose_rel_range(dvo_ctx* ctx, const dvo_pair_record* d_records, int pairs
 // -ffp-contract=off, so each product and sum rounds as written).
 int dvo_pose_chain_host(const double* T_rel, int n, double* T_carry, double* T_abs) {
     if (n < 0 || (n > 0 && (!T_rel || !T_carry || !T_abs))) return DVO_EINVAL;
+    if (n == 0) return DVO_OK;  // nothing to chain; T_carry may be NULL (as dvo_pose_chain)
     double t[16];
     std::memcpy(t, T_carry, sizeof(t));
     for (int p = 0; p < n; ++p) {

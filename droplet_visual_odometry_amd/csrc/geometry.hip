@@ -1269,16 +1269,26 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
 // hypotheses) by uniform loads, each lane counting those at or below its item (empty pairs repeat a
 // boundary and are counted through).  Packing the items leaves no lane idle where a pair's
 // hypotheses end (64-hypothesis blocks per pair left stage A at 0.61 and stage C at 0.24 of the
-// VALU lanes active, profiles/r05zz_pmc_f64.json).
+// VALU lanes active, profiles/r05zz_pmc_f64.json).  Past 8 boundaries (a run of empty pairs: pairs
+// whose loop already stopped, idle sets) each lane finishes with a binary search up to the last
+// pair of the wave, so no wave walks a long run of empty pairs one load at a time.
+static_assert(kSolveNT == 64, "wave_item_pair assumes one wave of 64 items per block");
 __device__ __forceinline__ int wave_item_pair(const int32_t* off, int pairs, int e0, int e) {
     int p = pair_of(off, pairs, e0);
-    const int pb = p;
-    for (int k = pb + 1; k <= pairs; ++k) {
+    const int lim = min(pairs, p + 8);
+    for (int k = p + 1; k <= lim; ++k) {
         const int b = off[k];
-        if (b > e0 + 63) break;
+        if (b > e0 + 63) return p;
         p += e >= b;
     }
-    return p;
+    if (lim == pairs || p < lim) return p;
+    int lo = p, hi = pair_of(off, pairs, e0 + 63);
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 // Stage A of every hypothesis of the round (one thread each), a 1-D grid over the round's items.

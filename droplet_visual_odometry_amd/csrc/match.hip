@@ -90,12 +90,22 @@ __device__ __forceinline__ int key_old(int k) { return ((k >> 13) << 16) | (k & 
 template <bool kFull>
 __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&A)[2][kMKs], int (&best)[2][16], int t0,
                                          int nt, int r, int h, int rowb, int nq) {
-    const float rbf = (float)rowb;  // + goff below: exact, loop-invariant (hoisted into registers)
+    // the accumulators start at the backward key base of their rows, 2^20 + row (exact,
+    // loop-invariant: the MFMA's C input), so they end as backward keys; forward keys add the train
+    // index and carry the row, a constant of each forward minimum, taken off at the end
+    const float rbf = (float)rowb;
+    acc_t rb0, rb1;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+        const int goff = (g & 3) + 8 * (g >> 2);
+        rb0[g] = rbf + (float)goff;
+        rb1[g] = rbf + (float)(32 + goff);
+    }
 #pragma unroll 1
     for (int tt = 0; tt < kMStage / 32; ++tt) {
         const int j = t0 + 32 * tt + r;
-        const float cf = (float)(j < nt ? kKeyBase + j : (1 << 30));
-        acc_t acc0 = {}, acc1 = {};
+        const float cf = (float)(j < nt ? j : (1 << 30));
+        acc_t acc0 = rb0, acc1 = rb1;
 #pragma unroll
         for (int ks = 0; ks < kMKs; ++ks) {
             const v4i B = btc[(32 * tt + r) * kMChunks + ((2 * ks + h) ^ (r & kChunkMask))];
@@ -108,7 +118,7 @@ __device__ __forceinline__ void nn_stage(const v4i* btc, int* cmin, const v4i (&
             const int goff = (g & 3) + 8 * (g >> 2);
             best[0][g] = min(best[0][g], key_add(acc0[g], cf));
             best[1][g] = min(best[1][g], key_add(acc1[g], cf));
-            int k0 = key_add(acc0[g], rbf + (float)goff), k1 = key_add(acc1[g], rbf + (float)(32 + goff));
+            int k0 = __float_as_int(acc0[g]), k1 = __float_as_int(acc1[g]);
             if (!kFull) {
                 k0 = rowb - kKeyBase + goff < nq ? k0 : kKeyNone;
                 k1 = rowb - kKeyBase + 32 + goff < nq ? k1 : kKeyNone;
@@ -222,9 +232,9 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
             const int qr = qs + 32 * s2 + (g & 3) + 8 * (g >> 2) + 4 * h;
             if (r == g && qr < nq) {
                 if (tsplit > 1) {
-                    if (st0 < nst) atomicMin(&fwd[qr], key_old(key_value(vv)));
+                    if (st0 < nst) atomicMin(&fwd[qr], key_old(key_value(vv) - qr));
                 } else {
-                    fwd[qr] = nt > 0 ? key_old(key_value(vv)) : -1;
+                    fwd[qr] = nt > 0 ? key_old(key_value(vv) - qr) : -1;
                 }
             }
         }

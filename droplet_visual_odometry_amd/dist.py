@@ -101,7 +101,8 @@ class ShardedPoseStream:
         # the second exchange: T_rel of each rank's own pairs (dvo_pose_rel_range), gathered for rank 0's chain
         self.p0_local = sum(self.counts[:rank])
         self.T_send = torch.zeros((self.cap, 4, 4), dtype=torch.float64, device=self.device)
-        self.T_recv = torch.empty((world, self.cap, 4, 4), dtype=torch.float64, device=gdev)
+        # rank 0 gathers the shards (exchange_T); the others only send
+        self.T_recv = torch.empty((world if rank == 0 else 1, self.cap, 4, 4), dtype=torch.float64, device=gdev)
 
     @property
     def records(self):
@@ -142,12 +143,19 @@ class ShardedPoseStream:
         return recs, cp, cc
 
     def exchange_T(self):
-        """All-gather every rank's T_rel (T_send[:n_local]) and return the window's T_rel in pair
-        order, [window_pairs, 4, 4] on `device`."""
+        """Gather every rank's T_rel (T_send[:n_local]) to rank 0, the only rank that chains, and
+        return the window's T_rel in pair order there ([window_pairs, 4, 4] on `device`); None on
+        the other ranks.  One gather: rank 0 receives (world - 1) shards and no other rank
+        receives anything (an all-gather would send every shard to every rank)."""
         import torch
         import torch.distributed as dist
         send = self.T_send.cpu() if self.host_gather else self.T_send
-        dist.all_gather_into_tensor(self.T_recv.view(-1), send.view(-1), group=self.group)
+        if self.world == 1:
+            self.T_recv[0].copy_(send)
+        else:
+            dist.gather(send, list(self.T_recv.unbind(0)) if self.rank == 0 else None, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
         T = torch.cat([self.T_recv[r, :c] for r, c in enumerate(self.counts)])
         return T.to(self.device) if self.host_gather else T
 
@@ -212,6 +220,13 @@ class ShardedStreamRunner:
         self.nsub = [0] * self.S
         self.i = 0
         self.prime_steps = self.S * (self.D - 1)
+
+    def reset_pose(self, P0=None, T0=None):
+        """Carry-in of the whole pose stream: P_prev (3x4, default K[I|0]) on every rank's tail and
+        the absolute pose T0 (4x4, default identity) of rank 0's chain, before the next window."""
+        self.tail.reset(P0, None)
+        if self.chain is not None:
+            self.chain.reset(T0)
 
     def step(self, frames, c_prev, c_cur, wait_torch: bool = True):
         """wait_torch (default): order the library stream after work queued on

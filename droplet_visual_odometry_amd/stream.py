@@ -189,6 +189,11 @@ class FrameStream:
             if t is None:
                 raise RuntimeError("retired records that were not submitted through this FrameStream")
             out.append((t, int(pairs[i])))
+        if out:
+            # the retire kernels (records_kernel) writing these records are queued on the library's
+            # stream by the call that retired them: keep the tensors alive until they have run,
+            # whether or not the caller keeps the returned list (process() drops it)
+            self._hold(*[t for t, _ in out])
         return out
 
     def pose_tail_batch(self, records: torch.Tensor, pairs: int, corners_prev: torch.Tensor,
@@ -396,6 +401,12 @@ class HostPoseChain:
         self.pending = [None] * slots
         self.n = 0
         self.pool = concurrent.futures.ThreadPoolExecutor(max_workers=1)
+
+    def reset(self, T0=None):
+        """The absolute pose before the next submitted window (default identity); waits for the
+        windows already submitted, which chain on the old carry."""
+        self.wait()
+        self.carry[:] = np.asarray(np.eye(4) if T0 is None else T0, np.float64).reshape(16)
 
     def submit(self, T_rel: torch.Tensor):
         n = T_rel.shape[0]

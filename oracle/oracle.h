@@ -28,6 +28,7 @@ typedef struct {
 // ---- ORB (cv::ORB_create() defaults, nfeatures variable) -------------------
 int ora_orb_level_sizes(int w, int h, int nlevels, int* sizes /*2*nlevels*/);
 int ora_orb_features_per_level(int nfeatures, int nlevels, int* out);
+int ora_orb_level_scales(int nlevels, float* out);
 // Pyramid (unblurred when blurred==0, else after GaussianBlur(7x7, sigma 2)).
 // out: levels packed back to back, each w_l*h_l bytes.
 int ora_orb_pyramid(const uint8_t* img, int w, int h, int stride, int nlevels,

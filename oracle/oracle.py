@@ -79,6 +79,7 @@ def lib():
         sig = {
             "ora_orb_level_sizes": [_c, _c, _c, _i32p],
             "ora_orb_features_per_level": [_c, _c, _i32p],
+            "ora_orb_level_scales": [_c, _f32p],
             "ora_orb_pyramid": [_u8p, _c, _c, _c, _c, _c, _u8p],
             "ora_fast": [_u8p, _c, _c, _c, _c, _i32p, _c, _ip],
             "ora_retain_best": [_f32p, _c, _c, _i32p],
@@ -120,6 +121,14 @@ def level_sizes(w, h, nlevels=8):
     out = np.zeros(2 * nlevels, np.int32)
     lib().ora_orb_level_sizes(w, h, nlevels, out)
     return [(int(out[2 * l]), int(out[2 * l + 1])) for l in range(nlevels)]
+
+
+def level_scales(nlevels=8):
+    """The oracle's getScale per level (float32): keypoint coordinates of level l
+    are float32(n) * level_scales()[l] (orb.cpp computeKeyPoints)."""
+    out = np.zeros(nlevels, np.float32)
+    lib().ora_orb_level_scales(nlevels, out)
+    return out
 
 
 def features_per_level(nfeatures, nlevels=8):

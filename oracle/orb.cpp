@@ -740,6 +740,13 @@ int ora_orb_level_sizes(int w, int h, int nlevels, int* sizes) {
     return 0;
 }
 
+// getScale of levels 0..nlevels-1: the factor the oracle multiplies a level's
+// keypoint coordinates and sizes by (orb.cpp computeKeyPoints / KeyPoint scaling).
+int ora_orb_level_scales(int nlevels, float* out) {
+    for (int l = 0; l < nlevels; ++l) out[l] = get_scale(l);
+    return 0;
+}
+
 int ora_orb_features_per_level(int nfeatures, int nlevels, int* out) {
     std::vector<int> n = features_per_level(nfeatures, nlevels);
     for (int l = 0; l < nlevels; ++l) out[l] = n[l];

@@ -39,7 +39,7 @@ def _stream(W, H, F, blank):
     return frames, np.stack(corners), K
 
 
-def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, streams, out):
+def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, streams, out, T0=None):
     import faulthandler
     import sys
     import torch
@@ -65,6 +65,8 @@ def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, strea
     d_corners = torch.from_numpy(corners).to(dev)
     run = ddist.ShardedStreamRunner(W, H, K, NF, n_pairs, world, rank, MARKER_LEN, ctx=Context(0),
                                     streams=streams, host_gather=backend == "gloo")
+    if T0 is not None:
+        run.reset_pose(None, T0)
     got_rec, got_Trel, got_Tabs = [], [], []
     pending = []
 
@@ -91,13 +93,13 @@ def _worker(rank, world, port, backend, W, H, NF, n_pairs, windows, blank, strea
     dist.destroy_process_group()
 
 
-def _single_rank(ctx, W, H, NF, F, blank):
+def _single_rank(ctx, W, H, NF, F, blank, T0=None):
     import torch
     from droplet_visual_odometry_amd.stream import FrameStream
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     frames, corners, K = _stream(W, H, F, blank)
     fs = FrameStream(W, H, K, nfeatures=NF, max_frames=F, ctx=ctx)
-    fs.reset_pose()
+    fs.reset_pose(None, T0)
     rec = fs.process(torch.from_numpy(frames).cuda())
     dc = torch.from_numpy(corners).cuda()
     T_rel, T_abs = fs.pose_tail(dc[:-1], dc[1:], MARKER_LEN)
@@ -107,9 +109,9 @@ def _single_rank(ctx, W, H, NF, F, blank):
     return out
 
 
-def _check(gpu_ctx, out, ranks, W, H, NF, F, blank):
+def _check(gpu_ctx, out, ranks, W, H, NF, F, blank, T0=None):
     from droplet_visual_odometry_amd._native import PAIR_RECORD_DTYPE
-    want_rec, want_Trel, want_Tabs = _single_rank(gpu_ctx, W, H, NF, F, blank)
+    want_rec, want_Trel, want_Tabs = _single_rank(gpu_ctx, W, H, NF, F, blank, T0)
     st = np.frombuffer(want_rec, PAIR_RECORD_DTYPE)["status"]
     for b in blank:  # the blank frame's two pairs fail in the single-rank run too
         assert st[b - 1] != 0 and st[b] != 0
@@ -137,6 +139,20 @@ def test_sharded_stream_equals_single_rank(gpu_ctx, W, H, NF, n_pairs, windows, 
     out = mgr.dict()
     mp.spawn(_worker, args=(2, _free_port(), "gloo", W, H, NF, n_pairs, windows, blank, 1, out), nprocs=2, join=True)
     _check(gpu_ctx, out, 2, W, H, NF, F, blank)
+
+
+def test_sharded_stream_reset_pose_non_identity(gpu_ctx):
+    """ShardedStreamRunner.reset_pose seeds both halves of the split tail: every rank's P_prev and
+    rank 0's host chain, so a non-identity T0 carries into T_abs as in one rank's pose tail."""
+    import torch.multiprocessing as mp
+    from droplet_visual_odometry_amd.transformations import euler_matrix
+    T0 = euler_matrix(0.1, -0.2, 0.3)
+    T0[:3, 3] = (0.5, -1.25, 2.0)
+    n_pairs, windows = 5, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), "gloo", W, H, NF, n_pairs, windows, (), 1, out, T0), nprocs=2, join=True)
+    _check(gpu_ctx, out, 2, W, H, NF, n_pairs * windows + 1, (), T0)
 
 
 @pytest.mark.parametrize("W,H,NF", [(640, 480, 500), (1280, 720, 2000)])

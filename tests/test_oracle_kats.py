@@ -14,9 +14,10 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def test_kat1_keypoint_scale_arithmetic():
-    """Every logged ORB coordinate is float32(n) * float32(pow(double(1.2f), l))."""
-    from droplet_visual_odometry_amd.plan import level_scale
+def test_kat1_keypoint_scale_arithmetic(oracle_mod):
+    """Every logged ORB coordinate is float32(n) * the oracle's level scale
+    float32(pow(double(1.2f), l)) (ora_orb_level_scales: nothing from the product package)."""
+    scales = oracle_mod.level_scales(8)
     kat = json.load(open(os.path.join(HERE, "golden", "notes_kat1.json")))
     coords = [c for m in kat["matches"] for c in m["prev"] + m["cur"]]
     assert len(coords) == 40
@@ -29,7 +30,7 @@ def test_kat1_keypoint_scale_arithmetic():
                 return True
         return False
 
-    ours = sum(explained(v, level_scale) for v in coords)
+    ours = sum(explained(v, lambda l: scales[l]) for v in coords)
     naive = sum(explained(v, lambda l: np.float32(1.2 ** l)) for v in coords)
     assert ours == 40
     assert naive < 40  # the float32(1.2**l) hypothesis does not explain the log
@@ -43,11 +44,10 @@ def test_kat1_distances_are_hamming_integers():
 
 
 def test_oracle_keypoints_on_level_grid(oracle_mod, frames_640):
-    from droplet_visual_odometry_amd.plan import level_scale
     frames, _ = frames_640
     kps, desc = oracle_mod.detect_and_compute(frames[0], 500)
     assert len(kps) == 500 and desc.shape == (500, 32)
-    s = np.array([level_scale(int(o)) for o in kps["octave"]], np.float32)
+    s = oracle_mod.level_scales(8)[kps["octave"]]
     xl = np.rint(kps["x"] / s)
     np.testing.assert_array_equal(np.float32(xl) * s, kps["x"])
     np.testing.assert_array_equal(kps["size"], np.float32(31) * s)
@@ -352,3 +352,10 @@ def test_surf_restatement_invariants(oracle_mod):
     assert set(np.unique(k["octave"])) <= {0, 1, 2, 3}
     k2, d2 = oracle_mod.surf_detect_and_compute(frames[0], 800.0)
     assert len(k2) < len(k) and np.all(k2["response"] > 800)
+
+
+def test_product_level_scale_equals_oracle(oracle_mod):
+    """The product's host plan places keypoints with the oracle's level scales, bit for bit."""
+    from droplet_visual_odometry_amd.plan import level_scale
+    got = np.array([level_scale(l) for l in range(8)], np.float32)
+    assert got.tobytes() == oracle_mod.level_scales(8).tobytes()

@@ -48,3 +48,4 @@ def test_host_chain_rejects_null_arguments():
     lib = _native.load_library()
     assert lib.dvo_pose_chain_host(None, 3, None, None) != 0
     assert lib.dvo_pose_chain_host(None, -1, None, None) != 0
+    assert lib.dvo_pose_chain_host(None, 0, None, None) == 0  # empty chain: nothing read or written

@@ -11,7 +11,7 @@ out="$root/gpurun_out/prof"
 mkdir -p "$out"
 export TMPDIR=/tmp
 cd /tmp
-short="$WL --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
+short="$WL --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --config-legs none --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
 timeout -s KILL 170 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
   -d /tmp/pmc_${tag}_stall -o run --output-format csv -- python3 "$root/bench.py" $short "$@" > "$out/${tag}_pmc_stall.log" 2>&1
 python3 "$root/tools/pmc_summary.py" $(find /tmp/pmc_${tag}_stall -name '*counter_collection.csv') "$out/${tag}_pmc_stall.csv" > /dev/null

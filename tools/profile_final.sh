@@ -23,7 +23,7 @@ mkdir -p "$out"
 B=${B:-3072}
 S=${S:-2}
 SP=${SP:-1}  # the counter passes: one stream (rocprofv3 --pmc serialises dispatches; with two streams their cross-stream waits stalled it)
-side="--cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0"
+side="--cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0 --config-legs none"
 pass="$WL --batch $B --streams $SP --steps 1 --warmup 1 --runs 1 --no-profile $side"
 tree="{\"git\": \"${DVO_TREE:-unknown}\", \"source_hash\": \"$(cd "$root" && python3 -c 'from droplet_visual_odometry_amd.build import source_hash; print(source_hash())')\"}"
 if [ "$part" = merge ]; then

@@ -17,7 +17,7 @@ out="$root/gpurun_out/prof"
 mkdir -p "$out"
 # WL: workload flags for every pass (e.g. WL="--width 640 --height 480 --nfeatures 1000"); the merge then
 # needs DVO_PMC_CONFIG="640 480 1000" so bench.py finds the document for that workload
-short="$WL --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
+short="$WL --steps 1 --warmup 1 --streams 1 --cpu-seconds 0 --config-legs none --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile --batch 512"
 if [ "$part" = merge ]; then
   python3 "$root/tools/pmc_calibrate.py" "$out/${tag}_calib_known.jsonl" "$out/${tag}_calib_FETCH_SIZE.csv" "$out/${tag}_calib_WRITE_SIZE.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_calib_rdreq.csv" > /dev/null
   python3 "$root/tools/pmc_traffic.py" "$out/${tag}_pmc_FETCH_SIZE.csv" "$out/${tag}_pmc_WRITE_SIZE.csv" "$out/${tag}_pmc_sq.csv" "$out/${tag}_pmc_calibration.json" "$out/${tag}_pmc_traffic.json" 512 "$out/${tag}_pmc_rdreq.csv"
@@ -26,7 +26,7 @@ fi
 export TMPDIR=/tmp
 cd /tmp
 if [ "$part" = a ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/st_$tag -o run --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 "$@" > "$out/${tag}_bench_under_rocprof.log" 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/st_$tag -o run --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --config-legs none --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 "$@" > "$out/${tag}_bench_under_rocprof.log" 2>&1
   python3 "$root/tools/summarize_profile.py" $(find /tmp/st_$tag -name '*kernel_stats.csv') "$out/${tag}_kernel_stats.csv" > "$out/${tag}_kernel_stats.txt"
   for c in FETCH_SIZE WRITE_SIZE; do
     # batch 512: the counter passes serialise every dispatch; traffic per frame is what bench.py scales

@@ -8,7 +8,7 @@ root=$(pwd)
 mkdir -p "$root/gpurun_out/trace"
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/tr_$tag -o run --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0 --no-profile --runs 1 "$@" > "$root/gpurun_out/trace/${tag}.log" 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/tr_$tag -o run --output-format csv -- python3 "$root/bench.py" --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --pose-check-32 0 --config-legs none --no-profile --runs 1 "$@" > "$root/gpurun_out/trace/${tag}.log" 2>&1
 csv=$(find /tmp/tr_$tag -name '*kernel_trace.csv')
 python3 "$root/tools/trace_summary.py" $csv "$root/gpurun_out/trace/${tag}_summary.txt" > /dev/null
 python3 - $csv "$root/gpurun_out/trace/${tag}_trace.csv.gz" <<'PY'

@@ -7,7 +7,7 @@ root=$(pwd)
 mkdir -p "$root/gpurun_out/trace"
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/ovl_$tag -o run --output-format csv -- python3 "$root/bench.py" --steps 6 --warmup 2 --cpu-seconds 0 --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile "$@" > "$root/gpurun_out/trace/${tag}_ovl.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/ovl_$tag -o run --output-format csv -- python3 "$root/bench.py" --steps 6 --warmup 2 --cpu-seconds 0 --config-legs none --no-ref-equivalent --no-host-fed --tail-world 0 --dropin-seconds 0 --no-profile "$@" > "$root/gpurun_out/trace/${tag}_ovl.log" 2>&1
 python3 "$root/tools/trace_overlap.py" $(find /tmp/ovl_$tag -name '*kernel_trace.csv') "$root/gpurun_out/trace/${tag}_overlap.txt" > /dev/null
 python3 -c "
 import csv, gzip, sys
