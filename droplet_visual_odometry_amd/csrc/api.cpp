@@ -607,12 +607,12 @@ int merged_round(dvo_stream* s) {
     sp.nsets = s->nsets;
     sp.F = s->cfg.max_frames;
     bool any = false;
+    for (int r = 0; r < kRansacRounds; ++r) sp.bound[r] = kRansacBounds[r];  // indexed by round
     for (int k = 0; k < s->nsets; ++k) {
         auto& st = s->sets[k];
         const bool run = st.used && st.round < kRansacRounds;
         sp.round[k] = run ? st.round : -1;
         sp.npairs[k] = run ? st.pairs : 0;
-        sp.bound[k] = kRansacBounds[k];
         any |= run;
     }
     if (!any) return DVO_OK;
