@@ -656,6 +656,13 @@ bool sets_pending(const dvo_stream* s) {
 int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, int pitch, dvo_pair_record* d_rec,
                bool detect_only, int pair_step = 1, bool drain = true) {
     dvo_ctx* ctx = s->ctx;
+    if (!detect_only && !drain && s->nsets < kRansacRounds) {  // the first pipelined submit: grow the sets
+        // (before params_of: the parameter block carries the buffer pointers)
+        if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "pair sets occupied at the first submit");
+        int rc = alloc_sets(s, kRansacRounds);
+        if (rc) return rc;
+        s->next_set = 0;
+    }
     StreamParams P = params_of(s, d_frames, n, fstride, pitch);
     P.pair_step = pair_step;
     const int pairs = detect_only ? 0 : stream_pairs(P);
@@ -668,12 +675,6 @@ int run_stream(dvo_stream* s, const uint8_t* d_frames, int n, int64_t fstride, i
     s->retired = 0;
     s->last_has_pairs = false;  // set again when a batch retires: the pose tail reads its records
     const int F = s->cfg.max_frames;
-    if (pairs >= 1 && !drain && s->nsets < kRansacRounds) {  // the first pipelined submit: grow the sets
-        if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "pair sets occupied at the first submit");
-        int rc = alloc_sets(s, kRansacRounds);
-        if (rc) return rc;
-        s->next_set = 0;
-    }
     const int k = s->next_set;
     if (pairs >= 1 && s->sets[k].used) {  // the ring is full (cannot happen in lockstep): finish its oldest
         int rc;
