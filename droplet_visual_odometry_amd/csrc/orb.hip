@@ -251,6 +251,61 @@ __device__ __forceinline__ uint32_t rs_ky(int c) {
     return (256u - cy1) | (cy1 << 16);
 }
 
+// OpenCV 3.2's resize(INTER_LINEAR) taps of one destination word (the 3.2 table, api.cpp
+// resize_coefs_32: per column {sx, sx1, a0 | a1 << 16}): the same staged-window selectors as
+// rs_lane, the 11-bit weight pair as the dot2 operand (a0, a1 <= 2048).  Past xmax the table has
+// sx1 = sx, a1 = 0: the second byte is read and weighted 0.
+__device__ __forceinline__ RsLane rs_lane32(const int32_t* cxt, int x0, int dw, int sx0, int maxw) {
+    int i0[4];
+    uint32_t kw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int4 c = *reinterpret_cast<const int4*>(cxt + 4 * min(x0 + j, dw - 1));
+        i0[j] = c.x - sx0;
+        kw[j] = (uint32_t)c.z;
+    }
+    RsLane L;
+    L.wb0 = min(i0[0] >> 2, maxw - 3);
+    const int base = 4 * L.wb0;
+    L.sh = min(i0[0] - base, 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t r = (uint32_t)min(max(i0[j] - base - L.sh, 0), 6);
+        L.sel[j] = 0x0C000C00u | r | ((r + 1) << 16);
+        L.kw[j] = kw[j];
+    }
+    return L;
+}
+// One destination word in 3.2 semantics from staged source rows a (r0) and b (r1) and the row
+// weights b0 | b1 << 16: h = a0 s[sx] + a1 s[sx1] (HResizeLinear, exact in 32 bits), then per
+// column VResizeLinearVec_32s8u's SSE2 form ((mulhi(h0 >> 4, b0) + mulhi(h1 >> 4, b1) + 2) >> 2)
+// before column xs, FixedPtCast<int, uchar, 22> from there (resize_level_ocv32_kernel's arithmetic).
+__device__ __forceinline__ uint32_t rs_word32(const uint32_t* a, const uint32_t* b, const RsLane& L, uint32_t ky,
+                                              int x0, int xs) {
+    const uint32_t a0 = a[L.wb0], a1 = a[L.wb0 + 1], a2 = a[L.wb0 + 2];
+    const uint32_t b0 = b[L.wb0], b1 = b[L.wb0 + 1], b2 = b[L.wb0 + 2];
+    const uint32_t alo = __builtin_amdgcn_alignbyte(a1, a0, L.sh), ahi = __builtin_amdgcn_alignbyte(a2, a1, L.sh);
+    const uint32_t blo = __builtin_amdgcn_alignbyte(b1, b0, L.sh), bhi = __builtin_amdgcn_alignbyte(b2, b1, L.sh);
+    const int wy0 = (int)(ky & 0xFFFFu), wy1 = (int)(ky >> 16);
+    uint32_t out = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int h0 = (int)__builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(ahi, alo, L.sel[j])),
+                                                   as_u16x2(L.kw[j]), 0u, false);
+        const int h1 = (int)__builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(bhi, blo, L.sel[j])),
+                                                   as_u16x2(L.kw[j]), 0u, false);
+        int v;
+        if (x0 + j < xs)
+            v = ((((h0 >> 4) * wy0) >> 16) + (((h1 >> 4) * wy1) >> 16) + 2) >> 2;
+        else
+            v = (int)(((uint32_t)h0 * (uint32_t)wy0 + (uint32_t)h1 * (uint32_t)wy1 + (1u << 21)) >> 22);
+        out |= (uint32_t)min(255, max(0, v)) << (8 * j);
+    }
+    return out;
+}
+
+// kOcv32Sem: OpenCV 3.2's INTER_LINEAR pyramid (the 3.2 tables), same staging and tiles.
+template <bool kOcv32Sem>
 __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, int l, int gx) {
     __shared__ uint32_t tile[kRsLRows][kRsW];
     int item;
@@ -267,12 +322,19 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const uint8_t* src = level_ptr(P, f, l - 1);
     const int sp = level_pitch(P, l - 1);
     uint8_t* dst = P.buf.pyr + (int64_t)f * P.plan.pyr_stride + D.pyr_off;
-    const int32_t* cxt = P.buf.coef + D.xcoef_off;
-    const int32_t* cyt = P.buf.coef + D.ycoef_off;
+    const int32_t* cxt = kOcv32Sem ? P.buf.coef32 + D.l32_x : P.buf.coef + D.xcoef_off;
+    const int32_t* cyt = kOcv32Sem ? P.buf.coef32 + D.l32_y : P.buf.coef + D.ycoef_off;
     // source window of the tile (wave-uniform)
-    const int sx0 = coef_ofs(cxt[xa]) & ~3;
-    const int sy0 = coef_ofs(cyt[ty0]);
-    const int nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsLR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
+    int sx0, sy0, nr;
+    if constexpr (kOcv32Sem) {  // rows already clipped in the table
+        sx0 = cxt[4 * xa] & ~3;
+        sy0 = cyt[4 * ty0];
+        nr = cyt[4 * min(ty0 + 4 * kRsLR - 1, D.h - 1) + 1] - sy0 + 1;
+    } else {
+        sx0 = coef_ofs(cxt[xa]) & ~3;
+        sy0 = coef_ofs(cyt[ty0]);
+        nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsLR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
+    }
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
     {  // kRsLRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
         uint32_t v0[kRsLRows / 4], v1[kRsLRows / 4];
@@ -289,15 +351,31 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
         }
     }
     // this lane's taps (their latency overlaps the staging)
-    const RsLane L = rs_lane(cxt, x0, D.w, sx0, kRsW);
+    const RsLane L = kOcv32Sem ? rs_lane32(cxt, x0, D.w, sx0, kRsW) : rs_lane(cxt, x0, D.w, sx0, kRsW);
     __syncthreads();
     const int dy0 = ty0 + wid * kRsLR;
     if (dy0 >= D.h) return;
+    const bool full = x0 + 4 <= D.w;
+    if constexpr (kOcv32Sem) {
+#pragma unroll
+        for (int rr = 0; rr < kRsLR; ++rr) {
+            const int dy = dy0 + rr;
+            if (dy >= D.h) break;
+            const int4 cy = *reinterpret_cast<const int4*>(cyt + 4 * dy);  // wave-uniform
+            const uint32_t word = rs_word32(tile[cy.x - sy0], tile[cy.y - sy0], L, (uint32_t)cy.z, x0, D.l32_xs);
+            uint8_t* drow = dst + (int64_t)dy * D.pitch;
+            if (full) {
+                *reinterpret_cast<uint32_t*>(drow + x0) = word;
+            } else {
+                for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+            }
+        }
+        return;
+    } else {
     const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform (table padded to 8 rows)
     const int4 cz = *reinterpret_cast<const int4*>(cyt + dy0 + 4);
     const int cys[kRsLR] = {cy.x, cy.y, cy.z, cy.w, cz.x, cz.y, cz.z, cz.w};
     static_assert(kRsLR == 8, "two int4 row-coefficient loads");
-    const bool full = x0 + 4 <= D.w;
 #pragma unroll
     for (int rr = 0; rr < kRsLR; ++rr) {
         const int dy = dy0 + rr;
@@ -312,6 +390,7 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
             for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
         }
     }
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -321,7 +400,8 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
 // per destination column {sx, sx1, a0 | a1 << 16} (past xmax: sx1 = sx, a0 =
 // 2048, a1 = 0, the HResizeLinear tail S[sx] * 2048) and per row {r0, r1,
 // b0 | b1 << 16} with the rows already clipped.  One thread per output pixel
-// (a parity mode, not the bench path): the two source rows are L2-resident.
+// Tiny levels only (ratios past 1.25, where the staged tiles do not fit); the
+// pyramid of ORB-sized frames runs through resize_level_lds_kernel<true>.
 // The vertical pass takes the SSE2 form below column l32_xs, the scalar
 // FixedPtCast form from there on.
 __global__ __launch_bounds__(256) void resize_level_ocv32_kernel(StreamParams P, int l) {
@@ -1846,14 +1926,20 @@ hipError_t launch_orb_frames(const StreamParams& P, hipStream_t s, hipEvent_t* e
     // 32 * 1.25 + 2 rows <= kRsRows
     auto lds_ok = [&](int l) { return 4 * pl.L[l - 1].w <= 5 * pl.L[l].w && 4 * pl.L[l - 1].h <= 5 * pl.L[l].h; };
     for (int l = 1; l < pl.nlevels; ++l) {
+        const bool lds = lds_ok(l);
         if (pl.semantics == kOcv32) {
-            hipLaunchKernelGGL(resize_level_ocv32_kernel, dim3((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F),
-                               dim3(256), 0, s, P, l);
+            if (lds)  // the 3.2 tables through the same staged tiles
+                hipLaunchKernelGGL(resize_level_lds_kernel<true>,
+                                   dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) *
+                                        xcd_frames(F)),
+                                   dim3(256), 0, s, P, l, (pl.L[l].w + 255) / 256);
+            else
+                hipLaunchKernelGGL(resize_level_ocv32_kernel, dim3((pl.L[l].w + 63) / 64, (pl.L[l].h + 3) / 4, F),
+                                   dim3(256), 0, s, P, l);
             continue;
         }
-        const bool lds = lds_ok(l);
         if (lds)
-            hipLaunchKernelGGL(resize_level_lds_kernel,
+            hipLaunchKernelGGL(resize_level_lds_kernel<false>,
                                dim3((pl.L[l].w + 255) / 256 * ((pl.L[l].h + 4 * kRsLR - 1) / (4 * kRsLR)) * xcd_frames(F)),
                                dim3(256), 0, s, P, l, (pl.L[l].w + 255) / 256);
         else  // level pairs whose rounded sizes differ by more than 1.25x: tiny frames (8x8: levels 4->5, 6->7)
