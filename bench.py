@@ -362,16 +362,6 @@ def main():
     if not args.no_ref_equivalent:
         leg("reference_equivalent", ref_equivalent_leg, args, pool, corners, scene.K, ctx, value, recs,
             pipe.last_s0)
-    if not args.no_host_fed:
-        for f in fss:
-            f.set_profiling(False)
-        leg("host_fed", host_fed_leg, args, pool, pipe, n_windows, value)
-    if args.tail_world > 1:
-        for f in fss:
-            f.set_profiling(False)
-        leg(f"rank0_tail_world{args.tail_world}", rank0_tail_leg, args, pool, pipe, corners, n_windows,
-            scene.K, ctx)
-
     cpu = None
     pose_check = None
     pose_check_32 = None
@@ -409,17 +399,12 @@ def main():
         if args.pose_check_32 > 0 and "c3_ocv32" not in leg_names:
             pose_check_32 = pose_check_opencv32(pool, scene.K, N, args.max_iters, args.pose_check_32, ctx)
 
-    dropin = dropin_rate(pool, corners, scene.K, N, args.dropin_seconds) if args.dropin_seconds > 0 else None
-
-    # BASELINE's other configs and the OpenCV 3.2 semantics, each on its own streams after the headline's
-    # are released (never `value`)
+    # BASELINE's other configs and the OpenCV 3.2 semantics, each on two new library streams (never `value`).
+    # They run before the legs that use torch side streams: torch creates its stream pool (dozens of HIP
+    # streams) on first use, after which new library streams can share a hardware queue with each other and
+    # run serialised
     leg_names = [x for x in args.config_legs.split(",") if x and x != "none"]
     if leg_names:
-        for f in fss:
-            f.close()
-        del pipe, fss, pool, corners, T_rel, T_abs
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
         cfg_legs = {}
         for name in leg_names:
             try:
@@ -431,6 +416,18 @@ def main():
         if "c3_ocv32" in cfg_legs and "pose_check" in cfg_legs["c3_ocv32"]:
             pose_check_32 = cfg_legs["c3_ocv32"]["pose_check"]
         legs["configs"] = cfg_legs
+
+    if not args.no_host_fed:
+        for f in fss:
+            f.set_profiling(False)
+        leg("host_fed", host_fed_leg, args, pool, pipe, n_windows, value)
+    if args.tail_world > 1:
+        for f in fss:
+            f.set_profiling(False)
+        leg(f"rank0_tail_world{args.tail_world}", rank0_tail_leg, args, pool, pipe, corners, n_windows,
+            scene.K, ctx)
+
+    dropin = dropin_rate(pool, corners, scene.K, N, args.dropin_seconds) if args.dropin_seconds > 0 else None
 
     default_cfg = (W, H, N) == (1280, 720, 2000)
     out = {
@@ -474,7 +471,10 @@ def main():
             out["speedup_vs_cpu_same_mode"]["reference_equivalent"] = \
                 legs["reference_equivalent"]["speedup_vs_cpu_same_mode"]
         out["speedup_vs_cpu_same_mode"]["cpu_threads"] = cpu["cores"]
-    out["legs"] = legs  # last: the config legs' summaries end the line
+    cfg_l = legs.pop("configs", None)
+    if cfg_l is not None:
+        legs["configs"] = cfg_l
+    out["legs"] = legs  # last: the config legs' summaries end the line (the driver keeps the stdout tail)
     print(json.dumps(out), flush=True)
 
 
