@@ -286,18 +286,22 @@ def main():
 
     ctx = Context(local_rank)
     S = max(1, args.streams)
-    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
-           for _ in range(S)]
-    for f in fss[1:]:
-        f.share_pose(fss[0])  # one pose stream across the alternating batches
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     corners = torch.tensor(np.stack([scene.marker_corners(i) for i in range(pool_n)]), dtype=torch.float64,
                            device=dev)
-    T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-    T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-    fss[0].reset_pose()
-    pipe = Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
-    torch.cuda.synchronize()
+
+    def make_pipe():
+        fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
+               for _ in range(S)]
+        for f in fss[1:]:
+            f.share_pose(fss[0])  # one pose stream across the alternating batches
+        T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+        T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+        fss[0].reset_pose()
+        torch.cuda.synchronize()
+        return fss, Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
+
+    fss, pipe = make_pipe()
     n_windows = max(1, (pool_n - 1) // B)
 
     host_log = []
@@ -405,6 +409,12 @@ def main():
     # run serialised
     leg_names = [x for x in args.config_legs.split(",") if x and x != "none"]
     if leg_names:
+        # the headline's streams are released for the legs' and built again for the legs below
+        for f in fss:
+            f.close()
+        del fss, pipe, sync_all
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         cfg_legs = {}
         for name in leg_names:
             try:
@@ -416,6 +426,8 @@ def main():
         if "c3_ocv32" in cfg_legs and "pose_check" in cfg_legs["c3_ocv32"]:
             pose_check_32 = cfg_legs["c3_ocv32"]["pose_check"]
         legs["configs"] = cfg_legs
+        if not args.no_host_fed or args.tail_world > 1:
+            fss, pipe = make_pipe()
 
     if not args.no_host_fed:
         for f in fss:
