@@ -1073,7 +1073,10 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
 // row below a sub-tile go to the next one in a small list.  Keys are written in the band's
 // segment at the rows' running offsets (sub-tiles run in row order), and band_cnt gets each row's
 // (offset << 16 | count), rows past the level's last row (offset = the band's total, count 0).
-constexpr int kFwRows = 8;                      // output rows per sub-tile
+#ifndef DVO_FASTW_ROWS
+#define DVO_FASTW_ROWS 8
+#endif
+constexpr int kFwRows = DVO_FASTW_ROWS;         // output rows per sub-tile
 static_assert(kBandRows % kFwRows == 0, "sub-tiles tile a band");
 constexpr int kFwSub = kBandRows / kFwRows;     // sub-tiles per band
 constexpr int kFwWin = kFwRows + 8;             // staged image rows
@@ -1085,7 +1088,7 @@ constexpr int kFwCarryR = (kFwCarryW + 63) / 64;
 constexpr int kFwCand = kFwSR * 128;            // pixel candidates: every score pixel of the sub-tile
 constexpr int kFwWordCand = kFwSR * 32;         // compass word entries
 static_assert(kFwWin * kFtWords == kFwNewW + kFwCarryW, "staging covers the window");
-static_assert(kFwCarryR == kFwPf && kFwCarryW == kFwNewW, "carry and prefetch words share the lane offsets");
+static_assert(kFwCarryR <= kFwPf && kFwCarryW <= kFwNewW, "carry words use the prefetch lane offsets");
 #ifndef DVO_FASTW_WAVES_PER_EU
 #define DVO_FASTW_WAVES_PER_EU 6
 #endif
@@ -2000,7 +2003,11 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+#ifndef DVO_DESC_PRIO
+#define DVO_DESC_PRIO 0  // wave priority of describe_kernel (s_setprio): ahead of the other stream's FAST waves
+#endif
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
+    if constexpr (DVO_DESC_PRIO > 0) __builtin_amdgcn_s_setprio(DVO_DESC_PRIO);
     __shared__ __attribute__((aligned(16))) uint8_t patch[kDKB][kDPH + 2][kDPW];  // + 2 padding rows
     __shared__ __attribute__((aligned(16))) uint8_t icw[4][kICR][kICW];
     __shared__ float s_ang[kDKB], s_ca[kDKB], s_sa[kDKB];
