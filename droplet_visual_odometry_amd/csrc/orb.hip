@@ -585,9 +585,6 @@ __global__ __launch_bounds__(256) void blur_kernel(StreamParams P) {
 // ------------------------------------------------------------------------
 // FAST-9/16 over one band of kBandRows output rows.
 constexpr int kFastNT = 256;
-#ifndef DVO_FAST_WAVE
-#define DVO_FAST_WAVE 0  // 1: fast_wave_kernel (one wave per strip, no workgroup barriers)
-#endif
 #ifndef DVO_FAST_SEG_CALL
 #define DVO_FAST_SEG_CALL 8
 #endif
@@ -1060,304 +1057,6 @@ __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_ker
             outp[row_off[wid][sr - 1] + before] = ((uint32_t)sc[a] << 24) | ((uint32_t)(r0 + sr - 1) << 12) | (uint32_t)x;
         }
         __syncthreads();
-    }
-}
-
-// FAST with one wave per column strip (DVO_FAST_WAVE): the same tiles, output and arithmetic as
-// fast_strip_kernel, but a strip is walked by ONE wave in sub-tiles of kFwRows output rows, so no
-// phase ever waits at a workgroup barrier: each wave's compass -> segment test -> score -> NMS ->
-// output chain is its own, ordered by wave fences only, and the CU interleaves the chains of
-// ~20 resident waves instead of stalling four waves at every barrier of a shared tile.  The window
-// is [r0 - 4, r0 + kFwRows + 4) x 144 columns; its last 8 rows are carried to the next sub-tile
-// (every image byte fetched once) and the two score rows above it too; the corners of the score
-// row below a sub-tile go to the next one in a small list.  Keys are written in the band's
-// segment at the rows' running offsets (sub-tiles run in row order), and band_cnt gets each row's
-// (offset << 16 | count), rows past the level's last row (offset = the band's total, count 0).
-#ifndef DVO_FASTW_ROWS
-#define DVO_FASTW_ROWS 8
-#endif
-constexpr int kFwRows = DVO_FASTW_ROWS;         // output rows per sub-tile
-static_assert(kBandRows % kFwRows == 0, "sub-tiles tile a band");
-constexpr int kFwSub = kBandRows / kFwRows;     // sub-tiles per band
-constexpr int kFwWin = kFwRows + 8;             // staged image rows
-constexpr int kFwSR = kFwRows + 2;              // score rows [r0 - 1, r0 + kFwRows]
-constexpr int kFwNewW = kFwRows * kFtWords;     // words loaded per sub-tile
-constexpr int kFwPf = (kFwNewW + 63) / 64;
-constexpr int kFwCarryW = 8 * kFtWords;         // image words carried to the next sub-tile
-constexpr int kFwCarryR = (kFwCarryW + 63) / 64;
-constexpr int kFwCand = kFwSR * 128;            // pixel candidates: every score pixel of the sub-tile
-constexpr int kFwWordCand = kFwSR * 32;         // compass word entries
-static_assert(kFwWin * kFtWords == kFwNewW + kFwCarryW, "staging covers the window");
-static_assert(kFwCarryR <= kFwPf && kFwCarryW <= kFwNewW, "carry words use the prefetch lane offsets");
-#ifndef DVO_FASTW_WAVES_PER_EU
-#define DVO_FASTW_WAVES_PER_EU 6
-#endif
-__global__ __launch_bounds__(64, DVO_FASTW_WAVES_PER_EU) void fast_wave_kernel(StreamParams P, int nseg) {
-    int it;
-    const int f = xcd_frame_item(P.plan.total_strips * nseg, P.nframes, it);
-    if (f >= P.nframes) return;
-    const int strip = it / nseg, seg = it - strip * nseg;
-    int l = 0;
-    while (l + 1 < P.plan.nlevels && strip >= P.plan.L[l + 1].strip_base) ++l;
-    const LevelGeom& G = P.plan.L[l];
-    const int c = strip - G.strip_base;
-    const int per_seg = (G.nbands + nseg - 1) / nseg;
-    const int b_begin = seg * per_seg, b_end = min(G.nbands, b_begin + per_seg);
-    if (b_begin >= b_end) return;
-    const int w = G.w, h = G.h;
-    const int xs = kBorder + c * kFastTW, xe = min(xs + kFastTW, w - kBorder);
-    const int bx = xs - 7;
-    const int thr = P.plan.fast_threshold;
-    const uint8_t* src = level_ptr(P, f, l);
-    const int sp = level_pitch(P, l);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, h * sp, 0x00020000);
-    __shared__ __attribute__((aligned(16))) uint8_t img[kFwWin * kFtLW];
-    __shared__ __attribute__((aligned(16))) uint8_t sc[kFwSR * kFtLW];
-    __shared__ uint16_t cand[kFwCand + 64];      // + 64 spare slots (branch-free appends)
-    __shared__ uint16_t wlist[kFwWordCand + 64];
-    __shared__ uint16_t carry[2][kFtCarryList];
-    __shared__ uint32_t keep[kFwRows][4];
-    __shared__ int s_rb[kFwRows];  // keys of the band before each row of the sub-tile
-    const int lane = threadIdx.x;
-    const int xlast = min(xe, w - 4);
-    // compass lanes: LDS word 1 + (lane & 31) of score row 2 t + (lane >> 5)
-    const int c_col = 4 + 4 * (lane & 31), c_hi = xlast - bx + 1 - c_col;
-    const uint32_t c_vm = (c_col == 4 ? 0xFFFF0000u : 0xFFFFFFFFu) &
-                          (c_hi >= 4 ? 0xFFFFFFFFu : c_hi <= 0 ? 0u : (1u << (8 * c_hi)) - 1u);
-    const uint32_t c_vm4 = (c_vm & 1u) | ((c_vm >> 7) & 2u) | ((c_vm >> 14) & 4u) | ((c_vm >> 21) & 8u);
-    const uint32_t thr2 = (uint32_t)thr * 0x10001u;
-    const auto wave_sync = []() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    uint32_t creg[kFwCarryR], pf[kFwPf], screg = 0;
-    int voff[kFwPf];
-#pragma unroll
-    for (int k = 0; k < kFwPf; ++k) {
-        const int q = lane + 64 * k;
-        const int rr = q / kFtWords, wd = q - rr * kFtWords;
-        voff[k] = 4 * wd + rr * sp;
-    }
-    // sub-tiles [t_begin, t_end): rows of the segment's bands that exist
-    const int rows_end = h - kBorder;
-    const int t_begin = b_begin * kFwSub;
-    const int t_end = min(b_end * kFwSub, (rows_end - kBorder + kFwRows - 1) / kFwRows);
-    {  // prologue: window rows [r0 - 4, r0 + 4) -> carry registers, [r0 + 4, r0 + kFwRows + 4) -> prefetch
-        const int ylo = kBorder + t_begin * kFwRows - 4;
-#pragma unroll
-        for (int k = 0; k < kFwCarryR; ++k) {
-            const int q = lane + 64 * k;
-            creg[k] = q < kFwCarryW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[k], bx + ylo * sp, 0)
-                                    : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kFwPf; ++k) {
-            const int q = lane + 64 * k;
-            pf[k] = q < kFwNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[k], bx + (ylo + 8) * sp, 0)
-                                : 0u;
-        }
-    }
-    for (int q = lane; q < (kFwSR * kFtLW) / 16; q += 64) reinterpret_cast<uint4*>(sc)[q] = make_uint4(0, 0, 0, 0);
-    int ncar = 0, par = 0;   // corners carried into this sub-tile (wave-uniform), their list
-    int band_keys = 0;       // keys written so far in the current band
-    for (int t = t_begin; t < t_end; ++t) {
-        const int b = t / kFwSub, st = t - b * kFwSub;
-        const int r0 = kBorder + t * kFwRows;
-        const int r1 = min(r0 + kFwRows, rows_end);
-        const int nrows = r1 - r0;
-        const int item = G.band_base + b * G.ntx + c;
-        if (st == 0) band_keys = 0;
-        // ---- window: carried rows 0..7, new rows 8..; score rows 0, 1 carried (first sub-tile: zero)
-#pragma unroll
-        for (int k = 0; k < kFwCarryR; ++k) {
-            const int q = lane + 64 * k;
-            if (q < kFwCarryW) reinterpret_cast<uint32_t*>(img)[q] = creg[k];
-        }
-#pragma unroll
-        for (int k = 0; k < kFwPf; ++k) {
-            const int q = lane + 64 * k;
-            if (q < kFwNewW) reinterpret_cast<uint32_t*>(img)[kFwCarryW + q] = pf[k];
-        }
-        // score rows 0, 1 (LDS words 1..32 each: the score columns): carried, or zero in the first sub-tile
-        reinterpret_cast<uint32_t*>(sc)[(lane >> 5) * kFtWords + 1 + (lane & 31)] = t == t_begin ? 0u : screg;
-        for (int q = (2 * kFtLW) / 16 + lane; q < (kFwSR * kFtLW) / 16; q += 64)
-            reinterpret_cast<uint4*>(sc)[q] = make_uint4(0, 0, 0, 0);
-        if (lane < kFwRows * 4) keep[lane >> 2][lane & 3] = 0;
-        wave_sync();
-        // ---- next sub-tile: carried rows from LDS, new rows from HBM (in flight during this one)
-        if (t + 1 < t_end) {
-#pragma unroll
-            for (int k = 0; k < kFwCarryR; ++k) {
-                const int q = lane + 64 * k;
-                creg[k] = q < kFwCarryW ? reinterpret_cast<const uint32_t*>(img)[kFwNewW + q] : 0u;
-            }
-            const int ynew = r0 + kFwRows + 4;
-#pragma unroll
-            for (int k = 0; k < kFwPf; ++k) {
-                const int q = lane + 64 * k;
-                pf[k] = q < kFwNewW ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff[k], bx + ynew * sp, 0)
-                                    : 0u;
-            }
-        }
-        // ---- compass over the score rows this sub-tile computes
-        const int nsr = nrows + 2;
-        const int sr_lo = t == t_begin ? 0 : 2;
-        int n = 0, nw = 0, ncw = 0;
-        for (int sr = sr_lo + (lane >> 5); __builtin_amdgcn_readfirstlane(sr - (lane >> 5)) < nsr; sr += 2) {
-            const int base = (sr + 3) * kFtLW + c_col;
-            const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + base);
-            const uint32_t wc = wp[0], wl = wp[-1], wr = wp[1];
-            const uint32_t wu = wp[-3 * kFtWords], wd = wp[3 * kFtWords];
-            const uint32_t r0p = compass_pass(as_u16x2(__builtin_amdgcn_perm(0, wc, 0x0C020C00)),
-                                              as_u16x2(__builtin_amdgcn_perm(0, wu, 0x0C020C00)),
-                                              as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C020C00)),
-                                              as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C050C03)),
-                                              as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C030C01)), thr2);
-            const uint32_t r1p = compass_pass(as_u16x2(__builtin_amdgcn_perm(0, wc, 0x0C030C01)),
-                                              as_u16x2(__builtin_amdgcn_perm(0, wu, 0x0C030C01)),
-                                              as_u16x2(__builtin_amdgcn_perm(0, wd, 0x0C030C01)),
-                                              as_u16x2(__builtin_amdgcn_perm(wr, wc, 0x0C060C04)),
-                                              as_u16x2(__builtin_amdgcn_perm(wc, wl, 0x0C040C02)), thr2);
-            uint32_t b0, b1;
-            asm("v_pk_min_u16 %0, %1, %2" : "=v"(b0) : "v"(r0p), "v"(0x00010001u));
-            asm("v_pk_min_u16 %0, %1, %2" : "=v"(b1) : "v"(r1p), "v"(0x00010001u));
-            const uint32_t m2 = b0 | (b1 << 1);
-            const uint32_t msk = (m2 | (m2 >> 14)) & (sr < nsr ? c_vm4 : 0u);
-            const bool any = msk != 0;
-            const unsigned long long bal = __ballot(any);
-            const int to = nw + (int)lane_prefix(bal);
-            wlist[any ? to : kFwWordCand + lane] = (uint16_t)((base >> 2) | (msk << 12));
-            nw += __popcll(bal);
-        }
-        wave_sync();
-        // word entries -> pixel entries
-        for (int e0 = 0; e0 < nw; e0 += 64) {
-            const int e = e0 + lane;
-            const uint32_t ent = e < nw ? (uint32_t)wlist[e] : 0u;
-            const uint32_t msk = ent >> 12;
-            const int a0 = (int)(ent & 0xFFFu) << 2;
-            const uint32_t cn = (uint32_t)__popc(msk);
-            const unsigned long long q0 = __ballot(cn & 1u), q1 = __ballot(cn & 2u), q2 = __ballot(cn & 4u);
-            const int pre = n + (int)lane_prefix(q0) + 2 * (int)lane_prefix(q1) + 4 * (int)lane_prefix(q2);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const bool on = (msk >> k) & 1u;
-                const int to = pre + __popc(msk & ((1u << k) - 1u));
-                if (on) cand[to] = (uint16_t)(a0 + k);
-            }
-            n += __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
-        }
-        wave_sync();
-        // segment test; the j-th corner overwrites the j-th (already read) entry
-        for (int e0 = 0; e0 < n; e0 += 64) {
-            const int e = e0 + lane;
-            bool is_corner = false;
-            int a = 0;
-            if (e < n) {
-                a = cand[e];
-                const uint8_t* p = img + a;
-                const int v = p[0];
-                const uint32_t hi = (uint32_t)(v + thr), lo = (uint32_t)(v - thr);
-                uint32_t br = 0, dk = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t cv = p[kCdy[k] * kFtLW + kCdx[k]];
-                    br = __builtin_amdgcn_alignbit(br, hi - cv, 31);
-                    dk = __builtin_amdgcn_alignbit(dk, cv - lo, 31);
-                }
-                is_corner = has_run9(br) || has_run9(dk);
-            }
-            const unsigned long long bal = __ballot(is_corner);
-            cand[is_corner ? ncw + (int)lane_prefix(bal) : kFwCand + lane] = (uint16_t)a;
-            ncw += __popcll(bal);
-        }
-        wave_sync();
-        for (int e = lane; e < ncw; e += 64) {
-            const int a = cand[e];
-            sc[a - 3 * kFtLW] = (uint8_t)fast_score16_pk(img + a, kFtLW, thr);
-        }
-        // score rows kFwRows, kFwRows + 1 for the next sub-tile (final after the scores)
-        wave_sync();
-        screg = reinterpret_cast<const uint32_t*>(sc)[(kFwRows + (lane >> 5)) * kFtWords + 1 + (lane & 31)];
-        // ---- strict 3x3 NMS of the carried and new corners; the corners of score row kFwRows + 1
-        // are the next sub-tile's row-1 corners
-        int nnext = 0;
-        for (int e0 = 0; e0 < ncar + ncw; e0 += 64) {
-            const int e = e0 + lane;
-            bool to_next = false;
-            int a = 0;
-            if (e < ncar + ncw) {
-                a = (e < ncar ? (int)carry[par][e] : (int)cand[e - ncar]) - 3 * kFtLW;
-                const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
-                if (sr == kFwRows + 1) {
-                    to_next = true;
-                } else if (sr >= 1 && sr <= nrows && x >= xs && x < xe) {
-                    const uint8_t* s = sc + a;
-                    const uint32_t v = s[0];
-                    const uint32_t nmax = max(max(max((uint32_t)s[-kFtLW - 1], (uint32_t)s[-kFtLW]),
-                                                  max((uint32_t)s[-kFtLW + 1], (uint32_t)s[-1])),
-                                              max(max((uint32_t)s[1], (uint32_t)s[kFtLW - 1]),
-                                                  max((uint32_t)s[kFtLW], (uint32_t)s[kFtLW + 1])));
-                    if (v > nmax) {
-                        const int i_col = x - (xs - 1);
-                        atomicOr(&keep[sr - 1][i_col >> 5], 1u << (i_col & 31));
-                    }
-                }
-            }
-            const unsigned long long bal = __ballot(to_next);
-            if (to_next) carry[par ^ 1][nnext + (int)lane_prefix(bal)] = (uint16_t)(a + 3 * kFtLW - kFwRows * kFtLW);
-            nnext += __popcll(bal);
-        }
-        wave_sync();
-        // ---- output: this sub-tile's rows of the band's segment, after the band's earlier rows
-        uint32_t* outp = P.buf.band_cand + (int64_t)f * P.plan.band_cand_stride + G.band_cand_off +
-                         (int64_t)(b * G.ntx + c) * G.band_cap;
-        int32_t* cntp = P.buf.band_cnt + ((int64_t)f * P.plan.total_bands + item) * kBandRows;
-        int row_base;  // this lane's row (lane < kFwRows): keys before it in the band
-        int sub_total;
-        {
-            int rc = 0;
-            if (lane < kFwRows && lane < nrows)
-                rc = __popc(keep[lane][0]) + __popc(keep[lane][1]) + __popc(keep[lane][2]) + __popc(keep[lane][3]);
-            int incl = rc;
-#pragma unroll
-            for (int o = 1; o < kFwRows; o <<= 1) {
-                const int y2 = __shfl_up(incl, o);
-                if (lane >= o) incl += y2;
-            }
-            row_base = band_keys + incl - rc;
-            sub_total = __shfl(incl, kFwRows - 1);
-            if (lane < kFwRows) {
-                cntp[st * kFwRows + lane] = (row_base << 16) | rc;
-                s_rb[lane] = row_base;
-            }
-        }
-        wave_sync();
-        for (int e0 = 0; e0 < ncar + ncw; e0 += 64) {
-            const int e = e0 + lane;
-            if (e < ncar + ncw) {
-                const int a = (e < ncar ? (int)carry[par][e] : (int)cand[e - ncar]) - 3 * kFtLW;
-                const int sr = a / kFtLW, x = bx + (a - sr * kFtLW);
-                if (sr >= 1 && sr <= nrows && x >= xs && x < xe) {
-                    const int i_col = x - (xs - 1), wq = i_col >> 5;
-                    const uint32_t* kr = keep[sr - 1];
-                    if ((kr[wq] >> (i_col & 31)) & 1) {
-                        int before = __popc(kr[wq] & ((1u << (i_col & 31)) - 1));
-                        for (int q = 0; q < wq; ++q) before += __popc(kr[q]);
-                        outp[s_rb[sr - 1] + before] = ((uint32_t)sc[a] << 24) | ((uint32_t)(r0 + sr - 1) << 12) | (uint32_t)x;
-                    }
-                }
-            }
-        }
-        band_keys += sub_total;
-        // rows of the band past the level's last row: offset = the band's total, count 0
-        if (t + 1 == t_end && st + 1 < kFwSub) {
-            for (int rr = (st + 1) * kFwRows + lane; rr < kBandRows; rr += 64) cntp[rr] = band_keys << 16;
-        }
-        ncar = nnext;
-        par ^= 1;
-        wave_sync();
     }
 }
 
@@ -2003,11 +1702,7 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-#ifndef DVO_DESC_PRIO
-#define DVO_DESC_PRIO 0  // wave priority of describe_kernel (s_setprio): ahead of the other stream's FAST waves
-#endif
 __global__ __launch_bounds__(256) void describe_kernel(StreamParams P) {
-    if constexpr (DVO_DESC_PRIO > 0) __builtin_amdgcn_s_setprio(DVO_DESC_PRIO);
     __shared__ __attribute__((aligned(16))) uint8_t patch[kDKB][kDPH + 2][kDPW];  // + 2 padding rows
     __shared__ __attribute__((aligned(16))) uint8_t icw[4][kICR][kICW];
     __shared__ float s_ang[kDKB], s_ca[kDKB], s_sa[kDKB];
@@ -2256,15 +1951,9 @@ hipError_t launch_orb_frames(const StreamParams& P, hipStream_t s, hipEvent_t* e
     mark(ev, 1, 1, s);
 
     mark(ev, 2, 0, s);
-    if (pl.total_strips > 0) {
-#if DVO_FAST_WAVE
-        hipLaunchKernelGGL(fast_wave_kernel, dim3(pl.total_strips * kFastSeg(F) * xcd_frames(F)), dim3(64), 0, s, P,
-                           kFastSeg(F));
-#else
+    if (pl.total_strips > 0)
         hipLaunchKernelGGL(fast_strip_kernel, dim3(pl.total_strips * kFastSeg(F) * xcd_frames(F)), dim3(kFastNT), 0,
                            s, P, kFastSeg(F));
-#endif
-    }
     mark(ev, 2, 1, s);
     mark(ev, 3, 0, s);
     if (F <= kSelCallFrames)
