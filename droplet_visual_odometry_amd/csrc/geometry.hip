@@ -1367,13 +1367,9 @@ __global__ void dk_stats_kernel(int round, int nwaves) {
 #else
 #define DK_STAT(pass, n) ((void)0)
 #endif
-#ifndef DVO_PRIO_DK
-#define DVO_PRIO_DK 0  // wave priority (s_setprio) of ransac_dk_kernel
-#endif
 // 3 waves per SIMD (130 VGPRs); 4 spills 14 VGPRs and measured -0.3 % (profiles/r05s_ab_replay_dk_waves.txt)
 __global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
-    if constexpr (DVO_PRIO_DK > 0) __builtin_amdgcn_s_setprio(DVO_PRIO_DK);
     // pass 0: items [0, dk_ctl[1]) of the round's work list; pass k > 0: dk_list[k - 1][0, dk_ctl[1 + k])
     const int total = g.dk_ctl[1 + pass];
     if ((int)blockIdx.x * kDkNT >= total) return;

@@ -781,11 +781,7 @@ template <int kSeg>
 __device__ __forceinline__ int seg_at(const uint16_t* list, const int* cnt, int e) {
     return list[seg_index<kSeg>(cnt, e)];
 }
-#ifndef DVO_PRIO_FAST
-#define DVO_PRIO_FAST 0  // wave priority (s_setprio) of fast_strip_kernel against the other stream's kernels
-#endif
 __global__ __launch_bounds__(kFastNT, DVO_FAST_WAVES_PER_EU) void fast_strip_kernel(StreamParams P, int nseg) {
-    if constexpr (DVO_PRIO_FAST > 0) __builtin_amdgcn_s_setprio(DVO_PRIO_FAST);
     // nseg > 1 (batches of a few frames): a strip's tiles are walked by nseg workgroups,
     // segment k from tile k * ceil(nbands / nseg), each starting like tile 0 (2 more score rows)
     int it;
