@@ -534,7 +534,7 @@ int stream_alloc(dvo_stream* s) {
     // five-point records and parked Durand-Kerner lists of one merged round (a bound over any
     // number of sets: one set at each round)
     A(b.fprec, (size_t)std::max<int64_t>(round_blocks_bound(F, (int)hc), (int64_t)(hc + 63) / 64) * 128 * 64);
-    A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
+    A(b.dk_ctl, (size_t)kDkCtlInts);
     A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
     A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
@@ -1791,7 +1791,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 16, hc * 4, &dnmod)) || (rc = scratch(ctx, 17, hc * 40, &dcnt)) ||
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
-        (rc = scratch(ctx, 23, 4 * (2 + kDkMaxPasses), &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
+        (rc = scratch(ctx, 23, 4 * kDkCtlInts, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
         (rc = scratch(ctx, 62, 8, &daoff)) || (rc = scratch(ctx, 63, 8, &dsoff)) ||
         (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
         return rc;
