@@ -2107,7 +2107,7 @@ static hipError_t launch_round(const GeomArgs& g, const RoundSpec& spec, bool on
         const dim3 dgrid((unsigned)((w.items + kDkNT - 1) / kDkNT));
         for (int pass = 0; pass < kDkPasses; ++pass) {
             const int budget = pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30;
-            if (DVO_DK_REFILL && pass > 0) {
+            if (DVO_DK_REFILL && pass > 0 && (DVO_DK_REFILL == 1 || pass + 1 == kDkPasses)) {  // 2: last pass only
                 const unsigned nb = min(dgrid.x, (unsigned)kDkPersist);
                 hipLaunchKernelGGL(ransac_dk_refill_kernel, dim3(nb), dim3(kDkNT), 0, s, g, pass, budget,
                                    (int)nb * kDkNT);
