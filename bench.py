@@ -301,6 +301,7 @@ def main():
         torch.cuda.synchronize()
         return fss, Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
 
+    free0 = torch.cuda.mem_get_info(dev)[0]
     fss, pipe = make_pipe()
     n_windows = max(1, (pool_n - 1) // B)
 
@@ -318,6 +319,7 @@ def main():
     for i in range(prime):
         step(i)
     sync_all()
+    hbm_streams_gb = (free0 - torch.cuda.mem_get_info(dev)[0]) / 1e9  # the library streams after priming
     if not args.no_profile:
         for f in fss:
             f.set_profiling(True)
@@ -460,6 +462,7 @@ def main():
                    "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
                    "parallelism": "single GPU",
                    "streams_in_flight": S,
+                   "hbm_gb_library_streams": round(hbm_streams_gb, 2),
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0,
                    "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0,
