@@ -215,3 +215,37 @@ def test_sharded_one_stream_matches_single_rank_gloo(oracle_mod, n_pairs, window
         assert got.tobytes() == rec.tobytes()
     np.testing.assert_array_equal(np.frombuffer(out[0][1]).reshape(-1, 4, 4), want_Tr)
     np.testing.assert_array_equal(np.frombuffer(out[0][2]).reshape(-1, 4, 4), want_Ta)
+
+
+def _exchange_T_worker(rank, world, port, n_pairs, out):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = ddist.ShardedPoseStream(world, rank, n_pairs, "cpu", host_gather=True)
+    for w in range(2):  # two windows through the same buffers
+        T = torch.arange(sh.n_local * 16, dtype=torch.float64).reshape(-1, 4, 4) + 1000.0 * (sh.p0_local + 1) + w
+        sh.T_send[:sh.n_local].copy_(T)
+        got = sh.exchange_T()
+        out[(rank, w)] = None if got is None else got.numpy().tobytes()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_pairs", [(2, 7), (3, 8), (4, 3)])
+def test_exchange_T_gathers_to_rank0_only(world, n_pairs):
+    """The T_rel exchange of a sharded window (dist.ShardedPoseStream.exchange_T) is a gather to rank
+    0, the only rank that chains: rank 0 gets every rank's relative poses in global pair order (uneven
+    shards, a rank without pairs), the other ranks get nothing back."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_exchange_T_worker, args=(world, _free_port(), n_pairs, out), nprocs=world, join=True)
+    for w in range(2):
+        want = []
+        for r in range(world):
+            a, b = ddist.shard_pairs(n_pairs + 1, world, r)
+            want.append(np.arange((b - a) * 16, dtype=np.float64).reshape(-1, 4, 4) + 1000.0 * (a + 1) + w)
+        assert out[(0, w)] == np.concatenate(want).tobytes()
+        for r in range(1, world):
+            assert out[(r, w)] is None
