@@ -96,7 +96,7 @@ struct RansacState {
     int32_t pad[2];
 };
 constexpr int kDkMaxPasses = 4;  // Durand-Kerner passes per round (geometry.hip kDkBudgets)
-constexpr int kDkCtlInts = 2 + 2 * kDkMaxPasses;  // dk_ctl: -, pass-0 items, parked after pass k, taken in pass k
+constexpr int kDkCtlInts = 2 + kDkMaxPasses;  // dk_ctl: -, pass-0 items, parked after pass k
 // RANSAC rounds of a stream batch: round r solves hypotheses [bound[r-1], min(bound[r], niters)),
 // the last round everything left.  A batch's pairs take one round per dvo_stream_submit call
 // (the rounds of kRansacRounds consecutive batches run as ONE merged launch sequence), so a
@@ -226,7 +226,7 @@ struct GeomArgs {
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
     int32_t* a_off;         // [pairs + 1] 64-hypothesis blocks of the round before each pair
     int32_t* s_off;         // [pairs + 1] score blocks of the round before each pair
-    int32_t* dk_ctl;        // [kDkCtlInts] -, pass-0 items, parked after pass k, taken from pass k's list
+    int32_t* dk_ctl;        // [kDkCtlInts] -, pass-0 items, parked after pass k
     int32_t* dk_list;       // [kDkMaxPasses - 1][dk_list_cap] parked polynomials (work-list items)
     int64_t dk_list_cap;    // >= pairs * hyp_cap
     int hyp_cap;            // max(max_iters, 1)

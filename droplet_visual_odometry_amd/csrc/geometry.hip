@@ -1259,7 +1259,7 @@ __global__ __launch_bounds__(1024) void ransac_plan_kernel(GeomArgs g, int pairs
         g.s_off[pairs] = s_carry.z;
         g.dk_ctl[0] = 0;
         g.dk_ctl[1] = s_carry.x;  // pass 0 items
-        for (int k = 0; k < 2 * kDkMaxPasses; ++k) g.dk_ctl[2 + k] = 0;  // parked after / taken in pass k
+        for (int k = 0; k < kDkMaxPasses; ++k) g.dk_ctl[2 + k] = 0;  // parked after pass k
     }
 }
 
@@ -1426,102 +1426,6 @@ void ransac_dk_kernel(GeomArgs g, int pairs, int pass, int budget) {
             dk_store(R, roots);
             DK_STAT(pass, sweep + 1);
             return;
-        }
-    }
-}
-
-// Passes after the first with lane refill (DVO_DK_REFILL): a persistent grid (kDkPersist blocks)
-// takes the pass's list statically for its first gridDim x kDkNT items, then every wave refills its
-// finished lanes from a counter (one atomicAdd per refill, at >= kDkRefillMin free lanes), so a wave
-// no longer idles its finished lanes until its slowest polynomial is done (pass 1 ran with 0.70 of
-// its lanes active, pass 2 with 0.81: profiles/r05zz_dk_passes.txt).  Same sweeps, same parking,
-// same records: the roots are bit-identical whichever lane runs a polynomial and when.
-#ifndef DVO_DK_REFILL
-#define DVO_DK_REFILL 0
-#endif
-#ifndef DVO_DK_PERSIST
-#define DVO_DK_PERSIST 768  // 256 CUs x 3 workgroups (12 waves per CU at 3 waves per SIMD)
-#endif
-#ifndef DVO_DK_REFILL_MIN
-#define DVO_DK_REFILL_MIN 16
-#endif
-constexpr int kDkPersist = DVO_DK_PERSIST, kDkRefillMin = DVO_DK_REFILL_MIN;
-__global__ __launch_bounds__(kDkNT) __attribute__((amdgpu_waves_per_eu(3, 8)))
-void ransac_dk_refill_kernel(GeomArgs g, int pass, int budget, int first_items) {
-    const int total = g.dk_ctl[1 + pass];
-    int* taken = &g.dk_ctl[2 + kDkMaxPasses + pass];
-    const int32_t* list = g.dk_list + (int64_t)(pass - 1) * g.dk_list_cap;
-    __shared__ double s_saved[20 * kDkNT];
-    const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * kDkNT + threadIdx.x;
-    bool active = e < total;
-    if (__ballot(active) == 0) return;  // the counter's items start past this wave's static range
-    bool more = first_items < total;    // wave-uniform: the counter may still hold items
-    double c[11];
-    Cx roots[10];
-    DkBrent br;
-    br.saved = s_saved + threadIdx.x;
-    br.stride = kDkNT;
-    int item = 0, sweep = 0;
-    double* R = nullptr;
-    auto load = [&](int it) {
-        item = list[it];
-        R = item_record(g, item);
-#pragma unroll
-        for (int k = 0; k < 11; ++k) c[k] = R[(kRecC + k) * 64];
-#pragma unroll
-        for (int i = 0; i < 10; i++) roots[i] = Cx{R[(kRecRoots + 2 * i) * 64], R[(kRecRoots + 2 * i + 1) * 64]};
-#pragma unroll
-        for (int k = 0; k < 20; ++k) br.saved[k * br.stride] = R[(kRecSnap + k) * 64];
-        const int pk = (int)R[kRecNr * 64];
-        br.it = pk & 511;
-        br.saved_it = (pk >> 9) & 511;
-        br.power = 1 << ((pk >> 18) & 15);
-        br.target = (pk >> 22) & 511;
-        sweep = 0;
-    };
-    if (active) load(e);
-    for (;;) {
-        if (active) {
-            if (sweep == budget) {  // park for the next pass
-#pragma unroll
-                for (int i = 0; i < 10; i++) {
-                    R[(kRecRoots + 2 * i) * 64] = roots[i].re;
-                    R[(kRecRoots + 2 * i + 1) * 64] = roots[i].im;
-                }
-#pragma unroll
-                for (int k = 0; k < 20; ++k) R[(kRecSnap + k) * 64] = br.saved[k * br.stride];
-                R[kRecNr * 64] = (double)(br.it | br.saved_it << 9 | (31 - __clz(br.power)) << 18 | br.target << 22);
-                const int slot = atomicAdd(&g.dk_ctl[2 + pass], 1);
-                g.dk_list[(int64_t)pass * g.dk_list_cap + slot] = item;
-                active = false;
-            } else {
-                bool moved, same = false;
-                dk_sweep<false>(c, roots, moved, same);
-                ++sweep;
-                if (same) {  // coincident roots: stage C redoes this polynomial exactly
-                    R[kRecGeneric * 64] = 2.0;
-                    active = false;
-                } else if (br.step(roots, moved)) {
-                    dk_store(R, roots);
-                    active = false;
-                }
-            }
-        }
-        const unsigned long long fr = __ballot(!active);
-        const int nfree = __popcll(fr);
-        if (more && nfree >= kDkRefillMin) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(taken, nfree);
-            base = first_items + __shfl(base, 0);
-            const int it = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fr >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fr, 0u));
-            if (!active && it < total) {
-                load(it);
-                active = true;
-            }
-            more = base + nfree < total;
-        } else if (nfree == 64 && !more) {
-            break;
         }
     }
 }
@@ -2105,16 +2009,9 @@ static hipError_t launch_round(const GeomArgs& g, const RoundSpec& spec, bool on
                            pairs);
     } else {
         const dim3 dgrid((unsigned)((w.items + kDkNT - 1) / kDkNT));
-        for (int pass = 0; pass < kDkPasses; ++pass) {
-            const int budget = pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30;
-            if (DVO_DK_REFILL && pass > 0 && (DVO_DK_REFILL == 1 || pass + 1 == kDkPasses)) {  // 2: last pass only
-                const unsigned nb = min(dgrid.x, (unsigned)kDkPersist);
-                hipLaunchKernelGGL(ransac_dk_refill_kernel, dim3(nb), dim3(kDkNT), 0, s, g, pass, budget,
-                                   (int)nb * kDkNT);
-            } else {
-                hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass, budget);
-            }
-        }
+        for (int pass = 0; pass < kDkPasses; ++pass)
+            hipLaunchKernelGGL(ransac_dk_kernel, dgrid, dim3(kDkNT), 0, s, g, pairs, pass,
+                               pass + 1 < kDkPasses ? kDkBudgets[pass] : 1 << 30);
 #ifdef DVO_DK_STATS
         hipLaunchKernelGGL(dk_stats_kernel, dim3(1), dim3(1), 0, s, spec.round[0], (int)dgrid.x * (kDkNT / 64));
 #endif
