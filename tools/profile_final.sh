@@ -4,7 +4,7 @@
 #   a  rocprofv3 --kernel-trace --stats of the default bench (side legs off), then the
 #      FETCH_SIZE and WRITE_SIZE passes over the same bench at one timed step, each beside the
 #      known-bytes calibration kernels (tools/calib);
-#   b  the read-request-size pass (+ calibration), the SQ instruction pass, the stall pass, the
+#   b (= b1 + b2)  b1: the read-request-size pass (+ calibration), the SQ instruction pass, the stall pass, the
 #      f64 pass, the lane pass (SQ_THREAD_CYCLES_VALU / SQ_ACTIVE_INST_VALU: active lanes per VALU
 #      instruction) and a counter-free kernel trace for the Durand-Kerner per-pass durations;
 #   merge  -> gpurun_out/prof/<tag>_{pmc_traffic,pmc_f64,dk_passes}.json, each carrying the tree
@@ -52,12 +52,15 @@ if [ "$part" = a ]; then
     run_pass $c $c
     calib_pass $c $c
   done
-elif [ "$part" = b ]; then
+fi
+if [ "$part" = b ] || [ "$part" = b1 ]; then
   rq="TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
   run_pass rdreq $rq
   calib_pass rdreq $rq
   run_pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES
   run_pass stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT
+fi
+if [ "$part" = b ] || [ "$part" = b2 ]; then
   run_pass f64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES
   awk 'NR == 1 || /ransac_dk_kernel/' $(find /tmp/pmc_${tag}_f64 -name '*counter_collection.csv') > "$out/${tag}_f64_raw.csv"
   run_pass lanes SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES
