@@ -146,9 +146,6 @@ struct NnOperands {
 #ifndef DVO_MATCH_WAVES
 #define DVO_MATCH_WAVES 1
 #endif
-#ifndef DVO_MATCH_PF2
-#define DVO_MATCH_PF2 0  // 1: train stages prefetched two ahead (A/B)
-#endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DVO_MATCH_WAVES)))
 void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit) {
     __shared__ v4i bt[2][kMStage * kMChunks];
@@ -195,8 +192,9 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
     const int st0 = (int)((int64_t)nst_all * ts / tsplit), nst = (int)((int64_t)nst_all * (ts + 1) / tsplit);
     // a stage: 64 trains x 32 bytes, 8 bytes (chunks 4 qd .. 4 qd + 3) per thread
     const int tr = threadIdx.x >> 2, qd = threadIdx.x & 3;
-    auto load_stage = [&](int st) { return XT[(int64_t)min(st * kMStage + tr, nt - 1) * 4 + qd]; };  // clamped
-    auto store_stage = [&](uint2 v, int st, int b) {
+    uint2 v;
+    auto load_stage = [&](int st) { v = XT[(int64_t)min(st * kMStage + tr, nt - 1) * 4 + qd]; };  // clamped
+    auto store_stage = [&](int st, int b) {
         const bool in = st * kMStage + tr < nt;  // zero operands past nt
         constexpr int kPer = kMChunks / 4;       // chunks of this thread's 8 bytes
 #pragma unroll
@@ -207,44 +205,22 @@ void nn_mfma_kernel(StreamParams P, NnOperands O, int pairs, int nqb, int tsplit
         }
         if (threadIdx.x < kMStage) colmin[b][threadIdx.x] = 0x7FFFFFFF;
     };
-    if (st0 < nst) store_stage(load_stage(st0), st0, 0);
-#if DVO_MATCH_PF2
-    // the trains two stages ahead in registers (two register slots, the loop unrolled by two so each
-    // slot is a fixed register): a stage's global load has two stages of MFMAs to arrive
-    uint2 va = make_uint2(0, 0), vb = make_uint2(0, 0);
-    if (st0 + 1 < nst) va = load_stage(st0 + 1);
-    if (st0 + 2 < nst) vb = load_stage(st0 + 2);
-    __syncthreads();
-    auto step = [&](int st, uint2& vn) {  // vn holds stage st + 1; reloaded with st + 3
-        const int cur = (st - st0) & 1;
-        if (full) nn_stage<true>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
-        else nn_stage<false>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
-        if (st + 1 < nst) store_stage(vn, st + 1, cur ^ 1);
-        if (st + 3 < nst) vn = load_stage(st + 3);
-        __syncthreads();
-        const int t = st * kMStage + threadIdx.x;
-        if (threadIdx.x < kMStage && t < nt && colmin[cur][threadIdx.x] != 0x7FFFFFFF)
-            atomicMin(&bwd[t], key_old(key_value(colmin[cur][threadIdx.x])));
-    };
-    for (int st = st0; st < nst; st += 2) {
-        step(st, va);
-        if (st + 1 < nst) step(st + 1, vb);
+    if (st0 < nst) {
+        load_stage(st0);
+        store_stage(st0, 0);
     }
-#else
     __syncthreads();
     for (int st = st0; st < nst; ++st) {
         const int cur = (st - st0) & 1;
-        uint2 v = make_uint2(0, 0);
-        if (st + 1 < nst) v = load_stage(st + 1);
+        if (st + 1 < nst) load_stage(st + 1);
         if (full) nn_stage<true>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
         else nn_stage<false>(bt[cur], colmin[cur], A, best, st * kMStage, nt, r, h, rowb, nq);
-        if (st + 1 < nst) store_stage(v, st + 1, cur ^ 1);
+        if (st + 1 < nst) store_stage(st + 1, cur ^ 1);
         __syncthreads();
         const int t = st * kMStage + threadIdx.x;
         if (threadIdx.x < kMStage && t < nt && colmin[cur][threadIdx.x] != 0x7FFFFFFF)
             atomicMin(&bwd[t], key_old(key_value(colmin[cur][threadIdx.x])));
     }
-#endif
     // forward: minimum over the 32 lanes of each half (they hold the 32 columns)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
