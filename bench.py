@@ -405,31 +405,25 @@ def main():
         if args.pose_check_32 > 0 and "c3_ocv32" not in leg_names:
             pose_check_32 = pose_check_opencv32(pool, scene.K, N, args.max_iters, args.pose_check_32, ctx)
 
-    # BASELINE's other configs and the OpenCV 3.2 semantics, each on two new library streams (never `value`).
-    # They run before the legs that use torch side streams: torch creates its stream pool (dozens of HIP
-    # streams) on first use, after which new library streams can share a hardware queue with each other and
-    # run serialised
+    # BASELINE's other configs and the OpenCV 3.2 semantics, each on two new library streams beside the
+    # headline's (never `value`).  They run before the legs that use torch side streams: torch creates its
+    # stream pool (dozens of HIP streams) on first use, after which new library streams can share a hardware
+    # queue with each other and run serialised
     leg_names = [x for x in args.config_legs.split(",") if x and x != "none"]
     if leg_names:
-        # the headline's streams are released for the legs' and built again for the legs below
-        for f in fss:
-            f.close()
-        del fss, pipe, sync_all
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
         cfg_legs = {}
         for name in leg_names:
             try:
                 cfg_legs[name] = config_leg(args, ctx, dev, name)
             except Exception as e:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
                 cfg_legs[name] = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
         if "c3_ocv32" in cfg_legs and "pose_check" in cfg_legs["c3_ocv32"]:
             pose_check_32 = cfg_legs["c3_ocv32"]["pose_check"]
         legs["configs"] = cfg_legs
-        if not args.no_host_fed or args.tail_world > 1:
-            fss, pipe = make_pipe()
 
     if not args.no_host_fed:
         for f in fss:

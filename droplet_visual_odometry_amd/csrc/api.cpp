@@ -455,6 +455,14 @@ GeomArgs geom_set(const GeomArgs& g, int k, int F, int64_t hc) {
 // Row pitch of the internal frame slab (word-aligned rows for the byte kernels).
 int frame_pitch(const dvo_stream* s) { return (s->cfg.width + 15) & ~15; }
 
+// The stream's frame slab (max_frames images at frame_pitch), allocated by the first call that
+// stages frames in it: host uploads (dvo_stream_pair, the per-call detector), realigned device
+// frames, undistorted frames.  Device-resident, word-aligned batches never need it.
+int frame_slab(dvo_stream* s) {
+    if (s->d_frames) return DVO_OK;
+    return dalloc(s, &s->d_frames, (size_t)s->cfg.max_frames * frame_pitch(s) * s->cfg.height);
+}
+
 // The per-pair geometry, one copy per pair set.  A stream starts with one set: the
 // drained calls (dvo_stream_process, _process_pairs, _pair) run a batch's rounds back to back
 // in it.  The first dvo_stream_submit / _submit_pairs grows it to kRansacRounds sets (the
@@ -515,11 +523,16 @@ int stream_alloc(dvo_stream* s) {
     b.blur = nullptr;  // the blurred pyramid (dvo_stream_get_pyramid(blurred) only): allocated on first use
     A(b.coef, (size_t)std::max(p.coef_total, 1));
     A(b.coef32, (size_t)std::max(p.coef32_total, 4));
-    A(b.band_cnt, (size_t)F * (p.total_bands + 1) * kBandRows);
-    A(b.band_cand, (size_t)F * p.band_cand_stride);
-    A(b.cand, (size_t)F * p.cand_stride);
-    A(b.resp, (size_t)F * p.cand_stride);
-    A(b.sel_tmp, (size_t)F * 2 * p.cand_stride);
+    // FAST survivors, candidate lists and selection scratch live only while their frame group is
+    // detected (launch_orb runs pyramid -> FAST -> selections -> Harris -> describe group by group,
+    // orb.hip frame_group): sized for the largest group, not the batch (at 1280x720, B 3072: 9.4
+    // instead of 37.5 GB per stream)
+    const int GF = orb_group_frames(F);
+    A(b.band_cnt, (size_t)GF * (p.total_bands + 1) * kBandRows);
+    A(b.band_cand, (size_t)GF * p.band_cand_stride);
+    A(b.cand, (size_t)GF * p.cand_stride);
+    A(b.resp, (size_t)GF * p.cand_stride);
+    A(b.sel_tmp, (size_t)GF * 2 * p.cand_stride);
     A(b.cnt1, (size_t)F * kMaxLevels);
     A(b.cnt2, (size_t)F * kMaxLevels);
     A(b.kps, (size_t)F * cap);
@@ -537,7 +550,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.dk_ctl, (size_t)kDkCtlInts);
     A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
-    A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
+    s->d_frames = nullptr;  // the frame slab: allocated by the first call that stages frames in it (frame_slab)
     A(s->d_carry, (size_t)28);
 #undef A
     return DVO_OK;
@@ -965,6 +978,7 @@ static int process_frames(dvo_stream* s, const uint8_t* d_frames, int n_frames, 
     HIP_TRY(hipSetDevice(ctx->device));
     if (((uintptr_t)d_frames | (uintptr_t)frame_stride | (uintptr_t)stride) & 3) {
         // the byte kernels read level 0 in 4-byte words: realign into the slab
+        if (int rc = frame_slab(s)) return rc;
         const int pw = frame_pitch(s);
         for (int i = 0; i < n_frames; ++i)
             HIP_TRY(hipMemcpy2DAsync(s->d_frames + (size_t)i * pw * s->cfg.height, pw, d_frames + i * frame_stride,
@@ -1055,6 +1069,7 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     if (!cur_img || !rec_out || stride < w || (!reuse_prev && !prev_img)) return fail(ctx, DVO_EINVAL, "bad image buffer");
     if (reuse_prev && !s->fc_valid) return fail(ctx, DVO_EINVAL, "reuse_prev needs a preceding dvo_stream_pair");
     if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "dvo_stream_pair: submitted batches are pending (dvo_stream_drain)");
+    if (int rc = frame_slab(s)) return rc;
     // the feature cache is valid only after a call that succeeds (a failing call may have left
     // its frame half-way through the rotation)
     s->fc_valid = false;
@@ -1263,6 +1278,7 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
         ctx->call_nf = params->nfeatures;
     }
     dvo_stream* s = ctx->call_stream;
+    if ((rc = frame_slab(s))) return rc;
     const int pw = frame_pitch(s);
     const size_t kc = (size_t)s->plan.kp_cap;
     Staging st;
@@ -2299,6 +2315,7 @@ int dvo_stream_process_undistorted(dvo_stream* s, dvo_undistort* u, const uint8_
     if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
     if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = frame_slab(s)) return rc;
     const int pw = frame_pitch(s);
     const int64_t fs = (int64_t)pw * s->cfg.height;
     HIP_TRY(launch_undistort_remap(u->U, u->d_xy, u->d_frac, d_frames, n_frames, frame_stride, stride, s->d_frames, fs,

@@ -318,6 +318,7 @@ inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
 // group (stages 0..4 of group g at group_ev[10 g ..]) instead of ev's stages 0..4.
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nullptr, hipEvent_t* group_ev = nullptr);
 int orb_groups(int nframes);
+int orb_group_frames(int nframes);
 // dvo_stream_pair's feature bookkeeping in one launch, per 4-byte word i of the frame-0 / frame-1 / cache
 // feature arrays (keypoints, descriptors, count, status): rotate = 1 (frame 0 holds the new current
 // frame): frame 1 <- frame 0, frame 0 <- cache, cache <- frame 0; rotate = 0: cache <- frame 1.
