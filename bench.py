@@ -900,9 +900,14 @@ def config_leg(args, ctx, dev, name):
     torch.cuda.synchronize()
     n_windows = 2
 
+    trace = os.environ.get("DVO_BENCH_TRACE") == "1"  # diagnostics: every step synchronised and logged
+
     def step(i):
         s0 = (i % n_windows) * B
         pipe.step(i % S, pool[s0:s0 + B + 1], s0)
+        if trace:
+            pipe.sync()
+            print(f"[{name}] step {i} ok ({time.perf_counter() - t_leg:.1f} s)", file=sys.stderr, flush=True)
 
     prime = max(args.warmup, pipe.prime_steps)
     for i in range(prime):
