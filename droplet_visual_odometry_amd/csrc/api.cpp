@@ -520,7 +520,7 @@ int stream_alloc(dvo_stream* s) {
     if ((rc = dalloc(s, &(ptr), (size_t)(n)))) \
         return rc;
     A(b.pyr, (size_t)F * p.pyr_stride);
-    b.blur = nullptr;  // the blurred pyramid (dvo_stream_get_pyramid(blurred) only): allocated on first use
+    A(b.blur, (size_t)F * p.blur_stride);  // the blurred pyramid (dvo_stream_get_pyramid(blurred) only)
     A(b.coef, (size_t)std::max(p.coef_total, 1));
     A(b.coef32, (size_t)std::max(p.coef32_total, 4));
     // FAST survivors, candidate lists and selection scratch live only while their frame group is
@@ -1228,10 +1228,6 @@ int dvo_stream_get_pyramid(dvo_stream* s, int frame, int level, int blurred, uin
     if (blurred) {
         // the detection path blurs only the descriptor windows (describe_kernel): the whole blurred
         // pyramid is recomputed here from the last call's frames, which must still be alive
-        if (!s->buf.blur) {
-            int rc = dalloc(s, &s->buf.blur, (size_t)s->cfg.max_frames * s->plan.blur_stride);
-            if (rc) return rc;
-        }
         HIP_TRY(launch_blur(params_of(s, s->last_frames, nfr, s->last_fstride, s->last_pitch), s->hs));
         HIP_TRY(hipStreamSynchronize(s->hs));
     }
