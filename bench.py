@@ -286,23 +286,18 @@ def main():
 
     ctx = Context(local_rank)
     S = max(1, args.streams)
+    fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
+           for _ in range(S)]
+    for f in fss[1:]:
+        f.share_pose(fss[0])  # one pose stream across the alternating batches
     from droplet_visual_odometry_amd.synth import MARKER_LEN
     corners = torch.tensor(np.stack([scene.marker_corners(i) for i in range(pool_n)]), dtype=torch.float64,
                            device=dev)
-
-    def make_pipe():
-        fss = [FrameStream(W, H, scene.K, nfeatures=N, max_frames=B + 1, max_iters=args.max_iters, ctx=ctx)
-               for _ in range(S)]
-        for f in fss[1:]:
-            f.share_pose(fss[0])  # one pose stream across the alternating batches
-        T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-        T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
-        fss[0].reset_pose()
-        torch.cuda.synchronize()
-        return fss, Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
-
-    free0 = torch.cuda.mem_get_info(dev)[0]
-    fss, pipe = make_pipe()
+    T_rel = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    T_abs = [torch.empty((B, 4, 4), dtype=torch.float64, device=dev) for _ in range(S)]
+    fss[0].reset_pose()
+    pipe = Pipeline(fss, B, corners, MARKER_LEN, T_rel, T_abs)
+    torch.cuda.synchronize()
     n_windows = max(1, (pool_n - 1) // B)
 
     host_log = []
@@ -319,7 +314,6 @@ def main():
     for i in range(prime):
         step(i)
     sync_all()
-    hbm_streams_gb = (free0 - torch.cuda.mem_get_info(dev)[0]) / 1e9  # the library streams after priming
     if not args.no_profile:
         for f in fss:
             f.set_profiling(True)
@@ -456,7 +450,6 @@ def main():
                    "width": W, "height": H, "nfeatures": N, "batch_frames": B, "max_iters": args.max_iters,
                    "parallelism": "single GPU",
                    "streams_in_flight": S,
-                   "hbm_gb_library_streams": round(hbm_streams_gb, 2),
                    "pairs_ok": f"{ok}/{len(recs)}", "mean_matches": round(m_avg, 1),
                    "mean_ransac_iters": round(float(np.mean(recs['ransac_iters'])), 1) if len(recs) else 0,
                    "mean_ransac_hypotheses_solved": round(float(np.mean(recs['n_hypotheses'])), 1) if len(recs) else 0,

@@ -455,14 +455,6 @@ GeomArgs geom_set(const GeomArgs& g, int k, int F, int64_t hc) {
 // Row pitch of the internal frame slab (word-aligned rows for the byte kernels).
 int frame_pitch(const dvo_stream* s) { return (s->cfg.width + 15) & ~15; }
 
-// The stream's frame slab (max_frames images at frame_pitch), allocated by the first call that
-// stages frames in it: host uploads (dvo_stream_pair, the per-call detector), realigned device
-// frames, undistorted frames.  Device-resident, word-aligned batches never need it.
-int frame_slab(dvo_stream* s) {
-    if (s->d_frames) return DVO_OK;
-    return dalloc(s, &s->d_frames, (size_t)s->cfg.max_frames * frame_pitch(s) * s->cfg.height);
-}
-
 // The per-pair geometry, one copy per pair set.  A stream starts with one set: the
 // drained calls (dvo_stream_process, _process_pairs, _pair) run a batch's rounds back to back
 // in it.  The first dvo_stream_submit / _submit_pairs grows it to kRansacRounds sets (the
@@ -550,7 +542,7 @@ int stream_alloc(dvo_stream* s) {
     A(b.dk_ctl, (size_t)kDkCtlInts);
     A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
-    s->d_frames = nullptr;  // the frame slab: allocated by the first call that stages frames in it (frame_slab)
+    A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
     A(s->d_carry, (size_t)28);
 #undef A
     return DVO_OK;
@@ -978,7 +970,6 @@ static int process_frames(dvo_stream* s, const uint8_t* d_frames, int n_frames, 
     HIP_TRY(hipSetDevice(ctx->device));
     if (((uintptr_t)d_frames | (uintptr_t)frame_stride | (uintptr_t)stride) & 3) {
         // the byte kernels read level 0 in 4-byte words: realign into the slab
-        if (int rc = frame_slab(s)) return rc;
         const int pw = frame_pitch(s);
         for (int i = 0; i < n_frames; ++i)
             HIP_TRY(hipMemcpy2DAsync(s->d_frames + (size_t)i * pw * s->cfg.height, pw, d_frames + i * frame_stride,
@@ -1069,7 +1060,6 @@ int dvo_stream_pair(dvo_stream* s, const uint8_t* prev_img, const uint8_t* cur_i
     if (!cur_img || !rec_out || stride < w || (!reuse_prev && !prev_img)) return fail(ctx, DVO_EINVAL, "bad image buffer");
     if (reuse_prev && !s->fc_valid) return fail(ctx, DVO_EINVAL, "reuse_prev needs a preceding dvo_stream_pair");
     if (sets_pending(s)) return fail(ctx, DVO_EINVAL, "dvo_stream_pair: submitted batches are pending (dvo_stream_drain)");
-    if (int rc = frame_slab(s)) return rc;
     // the feature cache is valid only after a call that succeeds (a failing call may have left
     // its frame half-way through the rotation)
     s->fc_valid = false;
@@ -1274,7 +1264,6 @@ int dvo_orb_detect_and_compute(dvo_ctx* ctx, const dvo_orb_params* params, const
         ctx->call_nf = params->nfeatures;
     }
     dvo_stream* s = ctx->call_stream;
-    if ((rc = frame_slab(s))) return rc;
     const int pw = frame_pitch(s);
     const size_t kc = (size_t)s->plan.kp_cap;
     Staging st;
@@ -2311,7 +2300,6 @@ int dvo_stream_process_undistorted(dvo_stream* s, dvo_undistort* u, const uint8_
     if (!d_frames || stride < s->cfg.width) return fail(ctx, DVO_EINVAL, "bad frame buffer");
     if (n_frames > 1 && !d_records) return fail(ctx, DVO_EINVAL, "null records");
     HIP_TRY(hipSetDevice(ctx->device));
-    if (int rc = frame_slab(s)) return rc;
     const int pw = frame_pitch(s);
     const int64_t fs = (int64_t)pw * s->cfg.height;
     HIP_TRY(launch_undistort_remap(u->U, u->d_xy, u->d_frac, d_frames, n_frames, frame_stride, stride, s->d_frames, fs,
