@@ -512,19 +512,14 @@ int stream_alloc(dvo_stream* s) {
     if ((rc = dalloc(s, &(ptr), (size_t)(n)))) \
         return rc;
     A(b.pyr, (size_t)F * p.pyr_stride);
-    A(b.blur, (size_t)F * p.blur_stride);  // the blurred pyramid (dvo_stream_get_pyramid(blurred) only)
+    A(b.blur, (size_t)F * p.blur_stride);
     A(b.coef, (size_t)std::max(p.coef_total, 1));
     A(b.coef32, (size_t)std::max(p.coef32_total, 4));
-    // FAST survivors, candidate lists and selection scratch live only while their frame group is
-    // detected (launch_orb runs pyramid -> FAST -> selections -> Harris -> describe group by group,
-    // orb.hip frame_group): sized for the largest group, not the batch (at 1280x720, B 3072: 9.4
-    // instead of 37.5 GB per stream)
-    const int GF = orb_group_frames(F);
-    A(b.band_cnt, (size_t)GF * (p.total_bands + 1) * kBandRows);
-    A(b.band_cand, (size_t)GF * p.band_cand_stride);
-    A(b.cand, (size_t)GF * p.cand_stride);
-    A(b.resp, (size_t)GF * p.cand_stride);
-    A(b.sel_tmp, (size_t)GF * 2 * p.cand_stride);
+    A(b.band_cnt, (size_t)F * (p.total_bands + 1) * kBandRows);
+    A(b.band_cand, (size_t)F * p.band_cand_stride);
+    A(b.cand, (size_t)F * p.cand_stride);
+    A(b.resp, (size_t)F * p.cand_stride);
+    A(b.sel_tmp, (size_t)F * 2 * p.cand_stride);
     A(b.cnt1, (size_t)F * kMaxLevels);
     A(b.cnt2, (size_t)F * kMaxLevels);
     A(b.kps, (size_t)F * cap);
@@ -539,7 +534,7 @@ int stream_alloc(dvo_stream* s) {
     // five-point records and parked Durand-Kerner lists of one merged round (a bound over any
     // number of sets: one set at each round)
     A(b.fprec, (size_t)std::max<int64_t>(round_blocks_bound(F, (int)hc), (int64_t)(hc + 63) / 64) * 128 * 64);
-    A(b.dk_ctl, (size_t)kDkCtlInts);
+    A(b.dk_ctl, (size_t)2 + kDkMaxPasses);
     A(b.dk_list, (size_t)(kDkMaxPasses - 1) * std::max<int64_t>(round_items_bound(F, (int)hc), (int64_t)hc));
     A(b.status, (size_t)F);
     A(s->d_frames, (size_t)F * frame_pitch(s) * s->cfg.height);
@@ -1792,7 +1787,7 @@ int dvo_find_essential_mat(dvo_ctx* ctx, const double* p1, const double* p2, int
         (rc = scratch(ctx, 16, hc * 4, &dnmod)) || (rc = scratch(ctx, 17, hc * 40, &dcnt)) ||
         (rc = scratch(ctx, 18, hc * 20, &dsub)) || (rc = scratch(ctx, 19, sizeof(RansacState), &drs)) ||
         (rc = scratch(ctx, 21, ((hc + 63) / 64) * 128 * 64 * 8, &drec)) || (rc = scratch(ctx, 22, 8, &doff)) ||
-        (rc = scratch(ctx, 23, 4 * kDkCtlInts, &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
+        (rc = scratch(ctx, 23, 4 * (2 + kDkMaxPasses), &dctl)) || (rc = scratch(ctx, 24, hc * 8, &dlist)) ||
         (rc = scratch(ctx, 62, 8, &daoff)) || (rc = scratch(ctx, 63, 8, &dsoff)) ||
         (rc = upload_points(ctx, st, p1, p2, m, &dpts)))
         return rc;

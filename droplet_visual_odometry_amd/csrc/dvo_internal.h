@@ -96,7 +96,6 @@ struct RansacState {
     int32_t pad[2];
 };
 constexpr int kDkMaxPasses = 4;  // Durand-Kerner passes per round (geometry.hip kDkBudgets)
-constexpr int kDkCtlInts = 2 + kDkMaxPasses;  // dk_ctl: -, pass-0 items, parked after pass k
 // RANSAC rounds of a stream batch: round r solves hypotheses [bound[r-1], min(bound[r], niters)),
 // the last round everything left.  A batch's pairs take one round per dvo_stream_submit call
 // (the rounds of kRansacRounds consecutive batches run as ONE merged launch sequence), so a
@@ -158,7 +157,7 @@ struct Buffers {
     int32_t* a_off;       // [sets F + 1] 64-hypothesis blocks before each pair (stage A / C, records)
     int32_t* s_off;       // [sets F + 1] score blocks before each pair
     PairHeader* hdr;      // [sets][F]
-    int32_t* dk_ctl;      // [kDkCtlInts]
+    int32_t* dk_ctl;      // [2 + kDkMaxPasses]
     int32_t* dk_list;     // [kDkMaxPasses - 1][F * hyp_cap] parked Durand-Kerner polynomials
     int32_t* status;      // [F] per-frame error flags
     double* E;            // [sets F][90]
@@ -226,7 +225,7 @@ struct GeomArgs {
     int32_t* dk_off;        // [pairs + 1] round work-list offsets
     int32_t* a_off;         // [pairs + 1] 64-hypothesis blocks of the round before each pair
     int32_t* s_off;         // [pairs + 1] score blocks of the round before each pair
-    int32_t* dk_ctl;        // [kDkCtlInts] -, pass-0 items, parked after pass k
+    int32_t* dk_ctl;        // [2 + kDkMaxPasses] -, pass-0 items, parked after pass k
     int32_t* dk_list;       // [kDkMaxPasses - 1][dk_list_cap] parked polynomials (work-list items)
     int64_t dk_list_cap;    // >= pairs * hyp_cap
     int hyp_cap;            // max(max_iters, 1)
@@ -318,7 +317,6 @@ inline void mark(hipEvent_t* ev, int stage, int end, hipStream_t s) {
 // group (stages 0..4 of group g at group_ev[10 g ..]) instead of ev's stages 0..4.
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev = nullptr, hipEvent_t* group_ev = nullptr);
 int orb_groups(int nframes);
-int orb_group_frames(int nframes);
 // dvo_stream_pair's feature bookkeeping in one launch, per 4-byte word i of the frame-0 / frame-1 / cache
 // feature arrays (keypoints, descriptors, count, status): rotate = 1 (frame 0 holds the new current
 // frame): frame 1 <- frame 0, frame 0 <- cache, cache <- frame 0; rotate = 0: cache <- frame 1.

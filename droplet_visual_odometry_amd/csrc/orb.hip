@@ -1978,8 +1978,7 @@ hipError_t launch_orb_frames(const StreamParams& P, hipStream_t s, hipEvent_t* e
 }
 
 // Frames [f0, f0 + n) of P as a batch of their own: every per-frame buffer the detection
-// kernels index by frame advanced by f0 frames, except the detection scratch, which holds one
-// group (api.cpp stream_alloc) and is reused by the next.
+// kernels index by frame advanced by f0 frames.
 StreamParams frame_group(const StreamParams& P, int f0, int n) {
     StreamParams Q = P;
     const Plan& pl = P.plan;
@@ -1988,7 +1987,11 @@ StreamParams frame_group(const StreamParams& P, int f0, int n) {
     Q.frames = P.frames + f * P.frame_stride;
     Q.buf.pyr += f * pl.pyr_stride;
     Q.buf.blur += f * pl.blur_stride;
-    // band_cnt, band_cand, cand, resp, sel_tmp: group-local (orb_group_frames frames), not advanced
+    Q.buf.band_cnt += f * pl.total_bands * kBandRows;
+    Q.buf.band_cand += f * pl.band_cand_stride;
+    Q.buf.cand += f * pl.cand_stride;
+    Q.buf.resp += f * pl.cand_stride;
+    Q.buf.sel_tmp += f * 2 * pl.cand_stride;
     Q.buf.cnt1 += f * kMaxLevels;
     Q.buf.cnt2 += f * kMaxLevels;
     Q.buf.kps += f * pl.kp_cap;
@@ -2015,13 +2018,6 @@ StreamParams frame_group(const StreamParams& P, int f0, int n) {
 int orb_groups(int nframes) {
     const int grp = DVO_ORB_GROUP;
     return grp > 0 && nframes > grp ? (nframes + grp - 1) / grp : 0;
-}
-// Frames of the largest detection group of any batch of at most `nframes` frames: a batch of
-// n <= DVO_ORB_GROUP frames is one group of n, a larger one splits into ceil(n / G) <= DVO_ORB_GROUP
-// frames per group ([n g / G, n (g + 1) / G)), so min(nframes, DVO_ORB_GROUP) bounds every call.
-int orb_group_frames(int nframes) {
-    const int grp = DVO_ORB_GROUP;
-    return grp > 0 && nframes > grp ? grp : nframes;
 }
 hipError_t launch_orb(const StreamParams& P, hipStream_t s, hipEvent_t* ev, hipEvent_t* group_ev) {
     const int F = P.nframes, G = orb_groups(F);
