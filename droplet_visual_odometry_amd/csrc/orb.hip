@@ -171,6 +171,9 @@ __global__ __launch_bounds__(256) void resize_level_kernel(StreamParams P, int l
 // coalesced word loads (lane k <- word k), then every lane reads its 3 words
 // per source row from LDS.  Same arithmetic as resize_level_kernel.
 constexpr int kRsLR = 8;  // output rows per wave (32 per workgroup)
+#ifndef DVO_RS_PIN
+#define DVO_RS_PIN 1
+#endif
 
 constexpr int kRsW = 96, kRsLRows = 44;  // 32 * 1.25 + 2 source rows, padded to a multiple of 4
 
@@ -335,6 +338,16 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
         sy0 = coef_ofs(cyt[ty0]);
         nr = min(coef_ofs(cyt[min(ty0 + 4 * kRsLR - 1, D.h - 1)]) + 1, S.h - 1) - sy0 + 1;
     }
+#if DVO_RS_PIN
+    // the lane's column taps and the wave's row taps are requested before the staging loads, so
+    // their latency overlaps it (dy0 is a multiple of 8: a wave with rows reads inside the row
+    // table's 8-row padding, an idle wave its last 8 rows)
+    const RsLane L = kOcv32Sem ? rs_lane32(cxt, x0, D.w, sx0, kRsW) : rs_lane(cxt, x0, D.w, sx0, kRsW);
+    const int dy0 = ty0 + wid * kRsLR;
+    const int dyc = min(dy0, ((D.h + 7) & ~7) - 8);
+    const int4 cy = *reinterpret_cast<const int4*>(cyt + dyc);
+    const int4 cz = *reinterpret_cast<const int4*>(cyt + dyc + 4);
+#endif
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
     {  // kRsLRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
         uint32_t v0[kRsLRows / 4], v1[kRsLRows / 4];
@@ -344,16 +357,24 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
             v0[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane, soff, 0);
             v1[it] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, sx0 + 4 * lane + 256, soff, 0);
         }
+#if DVO_RS_PIN
+        // keep every load in this one batch: the compiler otherwise sinks the first rows' second
+        // words into the lane < 32 store branch, a second memory round trip per workgroup
+#pragma unroll
+        for (int it = 0; it < kRsLRows / 4; ++it) asm volatile("" ::"v"(v1[it]));
+#endif
 #pragma unroll
         for (int it = 0; it < kRsLRows / 4; ++it) {
             tile[wid + 4 * it][lane] = v0[it];
             if (lane + 64 < kRsW) tile[wid + 4 * it][lane + 64] = v1[it];
         }
     }
+#if !DVO_RS_PIN
     // this lane's taps (their latency overlaps the staging)
     const RsLane L = kOcv32Sem ? rs_lane32(cxt, x0, D.w, sx0, kRsW) : rs_lane(cxt, x0, D.w, sx0, kRsW);
-    __syncthreads();
     const int dy0 = ty0 + wid * kRsLR;
+#endif
+    __syncthreads();
     if (dy0 >= D.h) return;
     const bool full = x0 + 4 <= D.w;
     if constexpr (kOcv32Sem) {
@@ -372,8 +393,10 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
         }
         return;
     } else {
+#if !DVO_RS_PIN
     const int4 cy = *reinterpret_cast<const int4*>(cyt + dy0);  // wave-uniform (table padded to 8 rows)
     const int4 cz = *reinterpret_cast<const int4*>(cyt + dy0 + 4);
+#endif
     const int cys[kRsLR] = {cy.x, cy.y, cy.z, cy.w, cz.x, cz.y, cz.z, cz.w};
     static_assert(kRsLR == 8, "two int4 row-coefficient loads");
 #pragma unroll
