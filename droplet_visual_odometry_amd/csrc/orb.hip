@@ -347,6 +347,11 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
     const int dyc = min(dy0, ((D.h + 7) & ~7) - 8);
     const int4 cy = *reinterpret_cast<const int4*>(cyt + dyc);
     const int4 cz = *reinterpret_cast<const int4*>(cyt + dyc + 4);
+    int4 r32[kOcv32Sem ? kRsLR : 1];  // the 3.2 row table {r0, r1, b0 | b1 << 16} of the wave's rows
+    if constexpr (kOcv32Sem) {
+#pragma unroll
+        for (int rr = 0; rr < kRsLR; ++rr) r32[rr] = *reinterpret_cast<const int4*>(cyt + 4 * min(dy0 + rr, D.h - 1));
+    }
 #endif
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), 0, S.h * sp, 0x00020000);
     {  // kRsLRows / 4 rows per wave, all loads in flight (rows past nr re-read row nr - 1: unused)
@@ -381,14 +386,21 @@ __global__ __launch_bounds__(256) void resize_level_lds_kernel(StreamParams P, i
 #pragma unroll
         for (int rr = 0; rr < kRsLR; ++rr) {
             const int dy = dy0 + rr;
-            if (dy >= D.h) break;
-            const int4 cy = *reinterpret_cast<const int4*>(cyt + 4 * dy);  // wave-uniform
-            const uint32_t word = rs_word32(tile[cy.x - sy0], tile[cy.y - sy0], L, (uint32_t)cy.z, x0, D.l32_xs);
-            uint8_t* drow = dst + (int64_t)dy * D.pitch;
-            if (full) {
-                *reinterpret_cast<uint32_t*>(drow + x0) = word;
-            } else {
-                for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+#if DVO_RS_PIN
+            if (dy < D.h) {  // (no break: the unrolled loop indexes r32 by constants)
+                const int4 cy = r32[rr];
+#else
+            {
+                if (dy >= D.h) break;
+                const int4 cy = *reinterpret_cast<const int4*>(cyt + 4 * dy);  // wave-uniform
+#endif
+                const uint32_t word = rs_word32(tile[cy.x - sy0], tile[cy.y - sy0], L, (uint32_t)cy.z, x0, D.l32_xs);
+                uint8_t* drow = dst + (int64_t)dy * D.pitch;
+                if (full) {
+                    *reinterpret_cast<uint32_t*>(drow + x0) = word;
+                } else {
+                    for (int j = 0; j < 4 && x0 + j < D.w; ++j) drow[x0 + j] = (uint8_t)(word >> (8 * j));
+                }
             }
         }
         return;
